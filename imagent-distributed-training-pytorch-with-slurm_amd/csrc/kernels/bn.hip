@@ -1,0 +1,353 @@
+// BatchNorm (training + eval) fused with residual add and ReLU, NHWC bf16.
+//
+// Replaces cuDNN/ATen native_batch_norm (+_backward), relu_ / threshold_
+// backward and the residual add of torchvision's BasicBlock/Bottleneck
+// (reference model at /root/reference/imagenet.py:312).
+//
+// Statistics: the per-channel (sum, sum of squares) of the BN input come from
+// the producing conv's epilogue (conv_igemm.hip, fp32 atomics), so the forward
+// is ONE streaming pass: read x (+ residual), write y.
+// Semantics follow nn.BatchNorm2d: biased variance to normalise, unbiased
+// variance into running_var, momentum 0.1, eps 1e-5, num_batches_tracked++.
+//
+// Backward is two streaming passes (reduce -> apply). The ReLU mask is taken
+// from the saved output y (y > 0), the residual gradient is the masked
+// upstream gradient. dgamma/dbeta are accumulated (fp32 atomics) straight into
+// the parameters' slots of the flat gradient arena.
+//
+// Layout: rows r = (n, h, w), C channels contiguous; each thread owns one
+// 16-B chunk (8 channels) of a row -> per-thread channel constants live in
+// registers, loads/stores are 16 B per lane (cdna_hip_programming.md G13).
+
+#include "common.h"
+
+namespace {
+
+struct Vec8 {
+    float v[8];
+};
+
+__device__ __forceinline__ Vec8 ld8(const bf16_t* p) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(p);
+    Vec8 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r.v[2 * i] = lo_bf(w[i]);
+        r.v[2 * i + 1] = hi_bf(w[i]);
+    }
+    return r;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const Vec8& x) {
+    u32x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf2(x.v[2 * i], x.v[2 * i + 1]);
+    *reinterpret_cast<u32x4*>(p) = w;
+}
+
+// mean / invstd from conv-epilogue sums
+__device__ __forceinline__ void mean_rstd(const float* sums, int C, int c, float inv_cnt, float eps,
+                                          float& mean, float& rstd) {
+    mean = sums[c] * inv_cnt;
+    const float var = fmaxf(sums[C + c] * inv_cnt - mean * mean, 0.f);
+    rstd = rsqrtf(var + eps);
+}
+
+// ---------------------------------------------------------------- forward
+// y = relu?( (x-mean)*rstd*g + b  [+ res | + (x2-mean2)*rstd2*g2 + b2] )
+template <int MODE, bool RELU>  // MODE 0: none, 1: identity residual, 2: second BN branch
+__global__ __launch_bounds__(256) void bn_fwd_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ sums, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const bf16_t* __restrict__ x2, const float* __restrict__ sums2,
+    const float* __restrict__ gamma2, const float* __restrict__ beta2, bf16_t* __restrict__ y,
+    float* __restrict__ save, float* __restrict__ save2, long R, int C, float inv_cnt, float eps,
+    int eval) {
+    const int cpr = C / 8;                // chunks per row
+    const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
+    const int tid = threadIdx.x;
+    if (tid >= rpb * cpr) return;
+    const int ch = tid % cpr, c0 = ch * 8;
+    float sc[8], sh[8], sc2[8], sh2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float mean, rstd;
+        if (eval) {  // sums holds running_mean / running_var
+            mean = sums[c0 + i];
+            rstd = rsqrtf(sums[C + c0 + i] + eps);
+        } else {
+            mean_rstd(sums, C, c0 + i, inv_cnt, eps, mean, rstd);
+        }
+        sc[i] = rstd * gamma[c0 + i];
+        sh[i] = beta[c0 + i] - mean * sc[i];
+        if (save && blockIdx.x == 0 && tid < cpr) {
+            save[c0 + i] = mean;
+            save[C + c0 + i] = rstd;
+        }
+        if (MODE == 2) {
+            float m2, r2;
+            if (eval) {
+                m2 = sums2[c0 + i];
+                r2 = rsqrtf(sums2[C + c0 + i] + eps);
+            } else {
+                mean_rstd(sums2, C, c0 + i, inv_cnt, eps, m2, r2);
+            }
+            sc2[i] = r2 * gamma2[c0 + i];
+            sh2[i] = beta2[c0 + i] - m2 * sc2[i];
+            if (save2 && blockIdx.x == 0 && tid < cpr) {
+                save2[c0 + i] = m2;
+                save2[C + c0 + i] = r2;
+            }
+        }
+    }
+    for (long r = (long)blockIdx.x * rpb + tid / cpr; r < R; r += (long)gridDim.x * rpb) {
+        const size_t off = (size_t)r * C + c0;
+        Vec8 v = ld8(x + off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v.v[i] = v.v[i] * sc[i] + sh[i];
+        if (MODE == 1) {
+            const Vec8 s = ld8(x2 + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] += s.v[i];
+        } else if (MODE == 2) {
+            const Vec8 s = ld8(x2 + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] += s.v[i] * sc2[i] + sh2[i];
+        }
+        if (RELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] = fmaxf(v.v[i], 0.f);
+        }
+        st8(y + off, v);
+    }
+}
+
+// running stats update + num_batches_tracked (one tiny launch per BN layer
+// would be wasteful: all layers of a step are updated by ONE launch over a
+// descriptor table, see imk_bn_running_update)
+struct RunDesc {
+    const float* sums;
+    float* rmean;
+    float* rvar;
+    long long* nbt;
+    int C;
+    float inv_cnt, unbias, momentum;
+};
+
+__global__ void bn_running_kernel(const RunDesc* __restrict__ d, int n) {
+    const RunDesc a = d[blockIdx.x];
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+        const float mean = a.sums[c] * a.inv_cnt;
+        const float var = fmaxf(a.sums[a.C + c] * a.inv_cnt - mean * mean, 0.f);
+        a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * mean;
+        a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * var * a.unbias;
+    }
+    if (threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+}
+
+// ---------------------------------------------------------------- backward
+// g = dy * (y > 0)   (RELU) ; per-channel sums  Sg = sum g,  Sgx = sum g * xhat
+// (MODE 2 also Sgx2 over the downsample branch x2 with its own statistics),
+// written to a zeroed fp32 scratch [3][C] with one atomic per channel per block.
+template <bool RELU, int MODE>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ save, const bf16_t* __restrict__ x2, const float* __restrict__ save2,
+    float* __restrict__ scratch, long R, int C) {
+    __shared__ float red[2048];  // [rpb][C], rpb*C == 2048
+    const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
+    const bool active = tid < rpb * cpr;
+    const int ch = tid % cpr, c0 = ch * 8, rsub = tid / cpr;
+    float mean[8], rstd[8], m2[8], r2[8];
+    float acc[3][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        mean[i] = save[c0 + i];
+        rstd[i] = save[C + c0 + i];
+        if (MODE == 2) {
+            m2[i] = save2[c0 + i];
+            r2[i] = save2[C + c0 + i];
+        }
+        acc[0][i] = acc[1][i] = acc[2][i] = 0.f;
+    }
+    if (active) {
+        for (long r = (long)blockIdx.x * rpb + rsub; r < R; r += (long)gridDim.x * rpb) {
+            const size_t off = (size_t)r * C + c0;
+            Vec8 g = ld8(dy + off);
+            if (RELU) {
+                const u32x4 yw = *reinterpret_cast<const u32x4*>(y + off);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
+                    if (!(hi_bf(yw[i]) > 0.f)) g.v[2 * i + 1] = 0.f;
+                }
+            }
+            const Vec8 xv = ld8(x + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                acc[0][i] += g.v[i] * (xv.v[i] - mean[i]) * rstd[i];
+                acc[1][i] += g.v[i];
+            }
+            if (MODE == 2) {
+                const Vec8 x2v = ld8(x2 + off);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc[2][i] += g.v[i] * (x2v.v[i] - m2[i]) * r2[i];
+            }
+        }
+    }
+    const int nq = MODE == 2 ? 3 : 2;
+#pragma unroll
+    for (int qi = 0; qi < 3; ++qi) {
+        if (qi >= nq) break;
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) red[rsub * C + c0 + i] = acc[qi][i];
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            float s = 0.f;
+            for (int rr = 0; rr < rpb; ++rr) s += red[rr * C + c];
+            atomicAdd(scratch + qi * C + c, s);
+        }
+    }
+}
+
+// dx = gamma*rstd*(g - Sg/R - xhat*Sgx/R); MODE 1 also writes the residual
+// gradient g, MODE 2 the downsample-branch input gradient. Block 0 also adds
+// the sums into the arena slots of dgamma/dbeta (+= : gradient accumulation).
+template <bool RELU, int MODE>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ scratch,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, const bf16_t* __restrict__ x2,
+    const float* __restrict__ save2, const float* __restrict__ gamma2, bf16_t* __restrict__ dx2,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
+    float* __restrict__ dbeta2, long R, int C, float inv_cnt) {
+    const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
+    if (blockIdx.x == 0) {
+        for (int c = tid; c < C; c += 256) {
+            if (dgamma) dgamma[c] += scratch[c];
+            if (dbeta) dbeta[c] += scratch[C + c];
+            if (MODE == 2) {
+                if (dgamma2) dgamma2[c] += scratch[2 * C + c];
+                if (dbeta2) dbeta2[c] += scratch[C + c];
+            }
+        }
+    }
+    if (tid >= rpb * cpr) return;
+    const int ch = tid % cpr, c0 = ch * 8;
+    float k1[8], k2[8], k3[8], mean[8], q1[8], q2[8], q3[8], m2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int c = c0 + i;
+        mean[i] = save[c];
+        const float rstd = save[C + c];
+        const float gr = gamma[c] * rstd;
+        k1[i] = gr;
+        k2[i] = -gr * inv_cnt * scratch[C + c];
+        k3[i] = -gr * inv_cnt * scratch[c] * rstd;
+        if (MODE == 2) {
+            m2[i] = save2[c];
+            const float rs2 = save2[C + c];
+            const float g2 = gamma2[c] * rs2;
+            q1[i] = g2;
+            q2[i] = -g2 * inv_cnt * scratch[C + c];
+            q3[i] = -g2 * inv_cnt * scratch[2 * C + c] * rs2;
+        }
+    }
+    for (long r = (long)blockIdx.x * rpb + tid / cpr; r < R; r += (long)gridDim.x * rpb) {
+        const size_t off = (size_t)r * C + c0;
+        Vec8 g = ld8(dy + off);
+        if (RELU) {
+            const u32x4 yw = *reinterpret_cast<const u32x4*>(y + off);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
+                if (!(hi_bf(yw[i]) > 0.f)) g.v[2 * i + 1] = 0.f;
+            }
+        }
+        const Vec8 xv = ld8(x + off);
+        Vec8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g.v[i] + k2[i] + k3[i] * (xv.v[i] - mean[i]);
+        st8(dx + off, o);
+        if (MODE == 1) st8(dres + off, g);
+        if (MODE == 2) {
+            const Vec8 x2v = ld8(x2 + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o.v[i] = q1[i] * g.v[i] + q2[i] + q3[i] * (x2v.v[i] - m2[i]);
+            st8(dx2 + off, o);
+        }
+    }
+}
+
+int grid_for(long R, int C) {
+    const int rpb = 256 / (C / 8);
+    long blocks = (R + rpb - 1) / rpb;
+    // >= 8 blocks per CU for streaming, then grid-stride (Guideline 11)
+    return (int)(blocks < 4096 ? blocks : 4096);
+}
+
+}  // namespace
+
+// mode: 0 plain, 1 + identity residual (x2), 2 + second BN branch (x2, sums2, gamma2, beta2)
+IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, const float* beta,
+                          const void* x2, const float* sums2, const float* gamma2, const float* beta2,
+                          void* y, float* save, float* save2, long R, int C, int mode, int relu,
+                          float eps, int eval, void* stream) {
+    if (C % 8 || C > 2048) return -100;
+    const float inv_cnt = 1.f / (float)R;
+    const int grid = grid_for(R, C);
+    hipStream_t st = (hipStream_t)stream;
+#define L(M, RL)                                                                                   \
+    hipLaunchKernelGGL((bn_fwd_kernel<M, RL>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
+                       gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, \
+                       R, C, inv_cnt, eps, eval)
+    if (mode == 0) { if (relu) L(0, true); else L(0, false); }
+    else if (mode == 1) { if (relu) L(1, true); else L(1, false); }
+    else { if (relu) L(2, true); else L(2, false); }
+#undef L
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_running_update(const void* descs, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(bn_running_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream,
+                       (const RunDesc*)descs, n);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
+
+// scratch: fp32 [3][C], zero-initialised by the caller.
+// mode 0: plain, 1: also dres (= masked dy, identity residual), 2: also dx2 (downsample BN branch)
+IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const float* save,
+                          const float* gamma, const void* x2, const float* save2,
+                          const float* gamma2, float* scratch, void* dx, void* dres, void* dx2,
+                          float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
+                          float* dbeta2_acc, long R, int C, int mode, int relu, void* stream) {
+    if (C % 8 || C > 2048) return -100;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = grid_for(R, C);
+    const int rgrid = grid < 1024 ? grid : 1024;
+#define LR(RL, M)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<RL, M>), dim3(rgrid), dim3(256), 0, st,               \
+                       (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, save, (const bf16_t*)x2, \
+                       save2, scratch, R, C)
+    if (relu) { if (mode == 2) LR(true, 2); else LR(true, 0); }
+    else { if (mode == 2) LR(false, 2); else LR(false, 0); }
+#undef LR
+    IMK_CHECK_LAUNCH();
+    const float inv_cnt = 1.f / (float)R;
+#define LA(RL, M)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
+                       (const bf16_t*)y, (const bf16_t*)x, save, gamma, scratch, (bf16_t*)dx,        \
+                       (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
+                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
+    if (relu) { if (mode == 0) LA(true, 0); else if (mode == 1) LA(true, 1); else LA(true, 2); }
+    else { if (mode == 0) LA(false, 0); else if (mode == 1) LA(false, 1); else LA(false, 2); }
+#undef LA
+    IMK_CHECK_LAUNCH();
+    return 0;
+}

@@ -1,0 +1,62 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels.
+// Wave = 64 lanes; MFMA 16x16x32 bf16 fragments; bf16 stored as raw u16.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // storage type (raw bits)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define WAVE 64
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+// Round-to-nearest-even via the hardware convert (v_cvt_pk_bf16_f32 on gfx950;
+// NaN stays NaN - MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): blocks that the dispatcher deals to the same XCD
+// (b % 8 equal) get a contiguous range of logical tile ids, so neighbouring
+// tiles that share operand panels hit the same 4 MiB L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    if (nwg <= 8) return orig;
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (orig >> 3);
+}
+
+#define IMK_EXPORT extern "C" __attribute__((visibility("default")))
+
+#define IMK_CHECK_LAUNCH()                         \
+    do {                                           \
+        hipError_t e_ = hipGetLastError();         \
+        if (e_ != hipSuccess) return (int)e_;      \
+    } while (0)

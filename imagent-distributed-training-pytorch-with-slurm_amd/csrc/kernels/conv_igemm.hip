@@ -1,0 +1,287 @@
+// MFMA implicit-GEMM convolution, NHWC bf16, for gfx950 (MI355X).
+//
+// Replaces cuDNN's conv fwd / dgrad kernels that the reference reaches via
+// torchvision resnet18 (/root/reference/imagenet.py:312, forward :123,
+// backward :128).
+//
+// ONE "gather GEMM" kernel serves the forward conv, the stride-1 dgrad, each
+// parity class of a strided dgrad (sub-pixel decomposition, no wasted MACs)
+// and the FC layer (a 1x1 conv on a 1x1 image):
+//
+//   out[pix(m)][n] = sum_{t < ntaps, c < C} X[gather(m, t)][c] * Wk[n][wtap(t)*C + c]
+//
+//   m      = (img, oh, ow) over the "row grid" OH x OW
+//   gather = (img, oh*sA + dh(t), ow*sA + dw(t))   (zero outside the image)
+//   pix    = (img, oh*sY + oy, ow*sY + ox)         (output pixel)
+//   taps   = a rectangle: t = (i, j), dh = dh0 + i*dhs, dw = dw0 + j*dws,
+//            weight tap = (kh0 + i*khs) * KW + (kw0 + j*kws)
+//
+//  * fwd:          sA = stride, dh0 = -pad, dhs = 1, taps = all KHxKW, Wk = W[Co][KH][KW][Ci]
+//  * dgrad (s=1):  X = dY, dh0 = pad, dhs = -1, Wk = W^T[Ci][KH][KW][Co]
+//  * dgrad (s>1):  one launch per output parity (ph, pw); only the taps with
+//                  kh == (ph + pad) mod s contribute, output pixel s*oh + ph.
+//
+// Tiling: 256 threads = 4 waves, block tile BM pixels x BN channels, BK = 64,
+// LDS double buffer with register staging (global_load_dwordx4 issued before
+// the MFMA phase, ds_write_b128 after it), rows padded by 16 B.
+// MFMA v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A operand and the
+// pixels as the B operand, so each lane's accumulator holds 4 consecutive
+// output CHANNELS of one pixel -> 8-byte NHWC stores without an LDS pass,
+// and BN statistics (sum, sum of squares per channel) reduce over the 16
+// lanes of a row group + one fp32 atomic per channel per wave.
+// Blocks are XCD-remapped so the channel tiles of one pixel panel share an L2.
+
+#include "common.h"
+
+struct IGemmArgs {
+    const bf16_t* X;   // gathered operand, NHWC [N][H][W][C]
+    const bf16_t* Wk;  // [Nout][ldb] bf16
+    void* Y;           // output NHWC, channel stride ldy
+    const float* bias; // [Nout] or null
+    float* stats;      // [2][Nout] (sum, sumsq) or null, fp32 atomics
+    int N, H, W, C;
+    int OH, OW, M;     // row grid, M = N*OH*OW
+    int Nout, ldb;
+    int sA;
+    int nth, ntw, dh0, dhs, dw0, dws, kh0, khs, kw0, kws, KW;
+    int YH, YW, sY, oy, ox, ldy;
+    int flags;         // bit0: output fp32 (else bf16); bit1: ReLU on output
+};
+
+#define IG_OUT_F32 1
+#define IG_RELU 2
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int LDK = BK + 8;  // padded row (elements): 144 B
+
+template <int BM, int BN, int WN, bool ALIGNED>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
+    constexpr int WM = 4 / WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    constexpr int A_CH = BM / 32, B_CH = BN / 32;  // 16-B chunks per thread per tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* sX = reinterpret_cast<bf16_t*>(smem);  // [2][BM][LDK]
+    bf16_t* sW = sX + 2 * BM * LDK;                // [2][BN][LDK]
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wn = wid % WN, wm = wid / WN;
+    const int nbn = (a.Nout + BN - 1) / BN;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bn = bid % nbn, bm = bid / nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int K = a.nth * a.ntw * a.C;
+    const int nk = (K + BK - 1) / BK;
+    const int col8 = tid & 7;
+    const int ohw = a.OH * a.OW;
+
+    // per-thread gather rows (fixed over the K loop)
+    const bf16_t* xrow[A_CH];
+    int ih0[A_CH], iw0[A_CH];
+    bool mok[A_CH];
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+        const int m = m0 + (tid >> 3) + 32 * i;
+        mok[i] = m < a.M;
+        const int mm = mok[i] ? m : 0;
+        const int img = mm / ohw, rem = mm - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        xrow[i] = a.X + (size_t)img * a.H * a.W * a.C;
+        ih0[i] = oh * a.sA;
+        iw0[i] = ow * a.sA;
+    }
+    const bf16_t* wrow[B_CH];
+    bool nok[B_CH];
+#pragma unroll
+    for (int j = 0; j < B_CH; ++j) {
+        const int n = n0 + (tid >> 3) + 32 * j;
+        nok[j] = n < a.Nout;
+        wrow[j] = a.Wk + (size_t)(nok[j] ? n : 0) * a.ldb;
+    }
+
+    u32x4 rx[A_CH], rw[B_CH];
+    auto load_tile = [&](int kt) {
+        const int k = kt * BK + col8 * 8;
+        int t, c;
+        if (ALIGNED) {  // C % 64 == 0: the whole K tile sits in one tap
+            t = (kt * BK) / a.C;
+            c = kt * BK - t * a.C + col8 * 8;
+        } else {
+            t = k / a.C;
+            c = k - t * a.C;
+        }
+        const bool kok = k < K;
+        const int ti = kok ? t / a.ntw : 0, tj = kok ? t - ti * a.ntw : 0;
+        const int dh = a.dh0 + ti * a.dhs, dw = a.dw0 + tj * a.dws;
+        const int wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+            const int ih = ih0[i] + dh, iw = iw0[i] + dw;
+            const bool ok = kok && mok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+            u32x4 v = {0, 0, 0, 0};
+            if (ok) v = *reinterpret_cast<const u32x4*>(xrow[i] + ((size_t)ih * a.W + iw) * a.C + c);
+            rx[i] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < B_CH; ++j) {
+            u32x4 v = {0, 0, 0, 0};
+            if (kok && nok[j]) v = *reinterpret_cast<const u32x4*>(wrow[j] + wtap * a.C + c);
+            rw[j] = v;
+        }
+    };
+    auto store_tile = [&](int buf) {
+        bf16_t* dx = sX + buf * BM * LDK;
+        bf16_t* dw = sW + buf * BN * LDK;
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i)
+            *reinterpret_cast<u32x4*>(dx + ((tid >> 3) + 32 * i) * LDK + col8 * 8) = rx[i];
+#pragma unroll
+        for (int j = 0; j < B_CH; ++j)
+            *reinterpret_cast<u32x4*>(dw + ((tid >> 3) + 32 * j) * LDK + col8 * 8) = rw[j];
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) {
+        load_tile(0);
+        store_tile(0);
+        __syncthreads();
+    }
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_tile(kt + 1);
+        const bf16_t* bx = sX + buf * BM * LDK + (wm * TM + fr) * LDK + fk;
+        const bf16_t* bw = sW + buf * BN * LDK + (wn * TN + fr) * LDK + fk;
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks) {
+            bf16x8 fw[FN], fx[FM];
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+                fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + ks * 32);
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+                fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + ks * 32);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[i], fx[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_tile(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---------------- epilogue ----------------
+    // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
+    const int nb = n0 + wn * TN + (lane >> 4) * 4;
+    const int mb = m0 + wm * TM + (lane & 15);
+    const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU;
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const int img = m / ohw, rem = m - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const size_t pix = ((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = nb + i * 16;
+            if (n >= a.Nout) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[i][j][r];
+                if (a.bias) v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
+                if (relu) v[r] = fmaxf(v[r], 0.f);
+            }
+            if (out_f32) {
+                float* y = reinterpret_cast<float*>(a.Y) + pix * a.ldy + n;
+                if (n + 3 < a.Nout && (a.ldy % 4) == 0) {
+                    *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
+                } else {
+                    for (int r = 0; r < 4; ++r)
+                        if (n + r < a.Nout) y[r] = v[r];
+                }
+            } else {
+                bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pix * a.ldy + n;
+                const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
+                if (n + 3 < a.Nout && (a.ldy % 4) == 0) {
+                    *reinterpret_cast<u32x2*>(y) = u32x2{lo, hi};
+                } else {
+                    const bf16_t h[4] = {(bf16_t)(lo & 0xffff), (bf16_t)(lo >> 16), (bf16_t)(hi & 0xffff),
+                                         (bf16_t)(hi >> 16)};
+                    for (int r = 0; r < 4; ++r)
+                        if (n + r < a.Nout) y[r] = h[r];
+                }
+                // statistics of the values BN will actually read (bf16-rounded)
+                v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
+            }
+            if (a.stats) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s1[i][r] += v[r];
+                    s2[i][r] += v[r] * v[r];
+                }
+            }
+        }
+    }
+    if (a.stats) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x1 = s1[i][r], x2 = s2[i][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    x1 += __shfl_xor(x1, o, 64);
+                    x2 += __shfl_xor(x2, o, 64);
+                }
+                const int n = nb + i * 16 + r;
+                if ((lane & 15) == 0 && n < a.Nout) {
+                    atomicAdd(a.stats + n, x1);
+                    atomicAdd(a.stats + a.Nout + n, x2);
+                }
+            }
+    }
+}
+
+template <int BM, int BN, int WN, bool AL>
+int launch(const IGemmArgs& a, hipStream_t st) {
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.Nout + BN - 1) / BN;
+    const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, WN, AL>), dim3(nbm * nbn), dim3(256), lds, st, a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace
+
+// Tile selection: BN follows Nout (64 -> 64-wide tiles, else 128), BM = 256/128.
+IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
+    const IGemmArgs& a = *args;
+    hipStream_t st = (hipStream_t)stream;
+    if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
+    if (a.M <= 0 || a.Nout <= 0) return 0;
+    const bool al = (a.C % BK) == 0;
+    if (tile == 0) tile = (a.Nout <= 64) ? 1 : 2;
+    switch (tile) {
+        case 1: return al ? launch<256, 64, 1, true>(a, st) : launch<256, 64, 1, false>(a, st);
+        case 2: return al ? launch<128, 128, 2, true>(a, st) : launch<128, 128, 2, false>(a, st);
+        case 3: return al ? launch<64, 128, 4, true>(a, st) : launch<64, 128, 4, false>(a, st);
+        default: return -101;
+    }
+}
+
+IMK_EXPORT int imk_igemm_args_size() { return (int)sizeof(IGemmArgs); }

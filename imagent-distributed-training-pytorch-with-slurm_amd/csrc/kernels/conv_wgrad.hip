@@ -1,0 +1,229 @@
+// MFMA implicit-GEMM weight gradient, NHWC bf16 in, fp32 out, for gfx950.
+//
+// Replaces cuDNN's conv wgrad that the reference runs inside
+// loss.backward() (/root/reference/imagenet.py:128), and fuses the DDP
+// bucket copy-in (K20): the fp32 result is accumulated straight into the
+// parameter's slot of the flat gradient arena that the RCCL all-reduce reads.
+//
+//   dW[co][tap*Ci + ci] += sum_m dY[m][co] * X[gather(m, tap)][ci]
+//   m = (img, oh, ow) over the conv's output grid, gather = forward gather.
+//
+// The reduction runs over the pixel index m (up to 12.8 M rows), which is the
+// OUTER (row) index of both NHWC operands. Tiles are staged row-major in LDS
+// ([m][channel]) with 16-B register-staged writes and consumed with gfx950's
+// transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10), so
+// no operand ever has to be transposed in memory. The k (= m) order inside an
+// MFMA fragment is permuted identically for both operands so that each
+// 32-lane half reads 8 CONSECUTIVE rows: with a 288-B row pitch (256 + 32)
+// those rows fall in disjoint 8-bank windows -> conflict-free reads.
+//
+// Split-K over m fills the chip (tiles x splits ~ 2-4 blocks per CU); partial
+// tiles are added with no-return fp32 atomics in 64-B row segments (the
+// chip-wide atomic rate, ~1.3 TB/s, is far above what these tiles need).
+// Index math for the gather uses host-computed magic-number division.
+
+#include "common.h"
+
+struct WgradArgs {
+    const bf16_t* dY;  // [M][Co]  (NHWC of the conv output)
+    const bf16_t* X;   // NHWC [N][H][W][Ci]
+    float* dW;         // [Co][KH*KW*Ci] fp32, accumulated (+=)
+    int N, H, W, Ci, Co;
+    int OH, OW, M;
+    int KH, KW, stride, pad;
+    int m_per_split;   // multiple of BR
+    uint32_t mg_ohw, sh_ohw, mg_ow, sh_ow;  // magic division by OH*OW and OW
+};
+
+namespace {
+
+constexpr int BR = 64;  // pixels (reduction rows) per stage
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
+    return (uint32_t)(((uint64_t)__umulhi(n, mg) + n) >> sh);
+}
+
+template <int BCO, int BKC, int WCO>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
+    constexpr int WKC = 4 / WCO;
+    constexpr int TCO = BCO / WCO, TKC = BKC / WKC;
+    constexpr int FN = TCO / 16, FM = TKC / 16;
+    constexpr int PCO = BCO * 2 + 32, PKC = BKC * 2 + 32;   // LDS row pitch, bytes
+    constexpr int CPR_D = BCO / 8, CPR_X = BKC / 8;         // 16-B chunks per row
+    constexpr int D_CH = BR * CPR_D / 256, X_CH = BR * CPR_X / 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sD = smem;                      // [2][BR][PCO]
+    char* sX = smem + 2 * BR * PCO;       // [2][BR][PKC]
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wco = wid % WCO, wkc = wid / WCO;
+    const int K = a.KH * a.KW * a.Ci;
+    const int nco = (a.Co + BCO - 1) / BCO, nkc = (K + BKC - 1) / BKC;
+    const int ntiles = nco * nkc;
+    const int bid = blockIdx.x;
+    const int tile = bid % ntiles, split = bid / ntiles;  // splits of one tile on one XCD group
+    const int tco = tile % nco, tkc = tile / nco;
+    const int co0 = tco * BCO, kc0 = tkc * BKC;
+    const int mbeg = split * a.m_per_split;
+    const int mend = min(a.M, mbeg + a.m_per_split);
+    if (mbeg >= mend) return;
+    const int nst = (mend - mbeg + BR - 1) / BR;
+
+    // fixed per-thread column chunk info
+    // dY chunks: id = tid + 256*i -> row id / CPR_D, col id % CPR_D (col fixed iff 256 % CPR_D == 0)
+    const int dcol = tid % CPR_D;
+    const int dco = co0 + dcol * 8;
+    const bool dco_ok = dco < a.Co;
+    const int xcol = tid % CPR_X;
+    const int xk = kc0 + xcol * 8;
+    const bool xk_ok = xk < K;
+    const int xtap = xk_ok ? xk / a.Ci : 0;
+    const int xci = xk - xtap * a.Ci;
+    const int xkh = xtap / a.KW, xkw = xtap - xkh * a.KW;
+    const int xdh = xkh - a.pad, xdw = xkw - a.pad;
+
+    u32x4 rd[D_CH], rx[X_CH];
+    auto load = [&](int st) {
+        const int mb = mbeg + st * BR;
+#pragma unroll
+        for (int i = 0; i < D_CH; ++i) {
+            const int row = (tid + 256 * i) / CPR_D;
+            const int m = mb + row;
+            u32x4 v = {0, 0, 0, 0};
+            if (m < mend && dco_ok) v = *reinterpret_cast<const u32x4*>(a.dY + (size_t)m * a.Co + dco);
+            rd[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < X_CH; ++i) {
+            const int row = (tid + 256 * i) / CPR_X;
+            const int m = mb + row;
+            u32x4 v = {0, 0, 0, 0};
+            if (m < mend && xk_ok) {
+                const uint32_t img = fdiv((uint32_t)m, a.mg_ohw, a.sh_ohw);
+                const uint32_t rem = (uint32_t)m - img * (uint32_t)(a.OH * a.OW);
+                const uint32_t oh = fdiv(rem, a.mg_ow, a.sh_ow);
+                const uint32_t ow = rem - oh * (uint32_t)a.OW;
+                const int ih = (int)oh * a.stride + xdh, iw = (int)ow * a.stride + xdw;
+                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                    v = *reinterpret_cast<const u32x4*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.Ci + xci);
+            }
+            rx[i] = v;
+        }
+    };
+    auto store = [&](int buf) {
+        char* d = sD + buf * BR * PCO;
+        char* x = sX + buf * BR * PKC;
+#pragma unroll
+        for (int i = 0; i < D_CH; ++i) {
+            const int id = tid + 256 * i;
+            *reinterpret_cast<u32x4*>(d + (id / CPR_D) * PCO + (id % CPR_D) * 16) = rd[i];
+        }
+#pragma unroll
+        for (int i = 0; i < X_CH; ++i) {
+            const int id = tid + 256 * i;
+            *reinterpret_cast<u32x4*>(x + (id / CPR_X) * PKC + (id % CPR_X) * 16) = rx[i];
+        }
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // tr-read lane addressing: 16-lane group g, lane 4q+p -> row q, cols 4p..4p+3.
+    // Fragment element e (0..7) of group g holds pixel row
+    //   e<4: 4g + e          e>=4: 16 + 4g + (e-4)     (same for both operands)
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row_a = 4 * g + q;          // first read
+    const int row_b = 16 + 4 * g + q;     // second read
+
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) load(st + 1);
+        const char* d = sD + buf * BR * PCO;
+        const char* x = sX + buf * BR * PKC;
+#pragma unroll
+        for (int ks = 0; ks < BR / 32; ++ks) {
+            bf16x8 fd[FN], fx[FM];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int col = wco * TCO + i * 16 + 4 * p;
+                const char* base = d + (ks * 32) * PCO + col * 2;
+                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_PTR(s16x4))(base + row_a * PCO));
+                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_PTR(s16x4))(base + row_b * PCO));
+                fd[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int col = wkc * TKC + j * 16 + 4 * p;
+                const char* base = x + (ks * 32) * PKC + col * 2;
+                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_PTR(s16x4))(base + row_a * PKC));
+                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_PTR(s16x4))(base + row_b * PKC));
+                fx[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+        }
+        if (st + 1 < nst) store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // acc[i][j][r]: co = co0 + wco*TCO + i*16 + (lane>>4)*4 + r ; k = kc0 + wkc*TKC + j*16 + (lane&15)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = co0 + wco * TCO + i * 16 + (lane >> 4) * 4 + r;
+            if (co >= a.Co) continue;
+            float* dst = a.dW + (size_t)co * K;
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+                const int k = kc0 + wkc * TKC + j * 16 + (lane & 15);
+                if (k < K) atomicAdd(dst + k, acc[i][j][r]);
+            }
+        }
+}
+
+template <int BCO, int BKC, int WCO>
+int launch(WgradArgs a, int splits, hipStream_t st) {
+    const int K = a.KH * a.KW * a.Ci;
+    const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
+    if (splits <= 0) {
+        // ~3 blocks per CU over 256 CUs, at least 4 stages per block
+        const int want = (768 + ntiles - 1) / ntiles;
+        const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
+        splits = max(1, min(want, maxs));
+    }
+    int mps = (a.M + splits - 1) / splits;
+    mps = (mps + BR - 1) / BR * BR;
+    splits = (a.M + mps - 1) / mps;
+    a.m_per_split = mps;
+    const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO>), dim3(ntiles * splits), dim3(256), lds, st, a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace
+
+IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
+    const WgradArgs& a = *args;
+    if (a.Ci % 8 || a.Co % 8) return -100;
+    if (a.M <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (a.Co <= 64) return launch<64, 128, 1>(a, splits, st);
+    return launch<128, 128, 2>(a, splits, st);
+}
+
+IMK_EXPORT int imk_wgrad_args_size() { return (int)sizeof(WgradArgs); }

@@ -1,0 +1,447 @@
+// Pooling, softmax cross-entropy + top-k, fused SGD, input normalisation and
+// weight re-layout kernels for gfx950 (MI355X). NHWC bf16 activations.
+//
+// Reference counterparts:
+//   K10/K11 max_pool2d_with_indices (+bwd)      -> maxpool_fwd / maxpool_bwd
+//   K12     adaptive_avg_pool2d (+bwd)          -> avgpool_fwd / avgpool_bwd
+//   K14-K16 log_softmax + nll_loss (+bwd), topk/eq/sum (accuracy(),
+//           /root/reference/imagenet.py:63-79, :124, :134) -> xent_fwd / xent_bwd
+//   K18     foreach SGD (imagenet.py:131, :325)  -> sgd_flat (one pass over
+//           the flat param/grad/momentum arenas, also refreshes the bf16 shadow)
+//   K21     ToTensor + Normalize (imagenet.py:280-283, CPU in the reference)
+//           -> normalize_u8 (uint8 HWC -> bf16 NHWC, optional crop / flip)
+//   K13     fc bias gradient -> colsum_bf16
+//   -       bf16 weight shadows: [Co][T][Ci] -> [Ci][T][Co] for dgrad (batched)
+
+#include "common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ maxpool
+// argmax stored per element as the in-window index (uint8), so the backward
+// is a gather over the <= ceil(k/s)^2 windows that contain an input pixel.
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H,
+                                                          int W, int C, int OH, int OW, int k, int s,
+                                                          int p) {
+    const int cpr = C / 8;
+    const long total = (long)N * OH * OW * cpr;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int ch = t % cpr;
+        long pix = t / cpr;
+        const int ow = pix % OW;
+        pix /= OW;
+        const int oh = pix % OH;
+        const int n = pix / OH;
+        float best[8];
+        int bi[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            best[i] = -INFINITY;
+            bi[i] = 0;
+        }
+        for (int dh = 0; dh < k; ++dh) {
+            const int ih = oh * s - p + dh;
+            if ((unsigned)ih >= (unsigned)H) continue;
+            for (int dw = 0; dw < k; ++dw) {
+                const int iw = ow * s - p + dw;
+                if ((unsigned)iw >= (unsigned)W) continue;
+                const u32x4 w =
+                    *reinterpret_cast<const u32x4*>(x + (((size_t)n * H + ih) * W + iw) * C + ch * 8);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float a = lo_bf(w[i]), b = hi_bf(w[i]);
+                    // strict > keeps the first maximum (torch semantics); NaN propagates
+                    if (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i])) { best[2 * i] = a; bi[2 * i] = dh * k + dw; }
+                    if (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1])) { best[2 * i + 1] = b; bi[2 * i + 1] = dh * k + dw; }
+                }
+            }
+        }
+        u32x4 o;
+        uint32_t i0 = 0, i1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = pack_bf2(best[2 * i], best[2 * i + 1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            i0 |= (uint32_t)bi[i] << (8 * i);
+            i1 |= (uint32_t)bi[4 + i] << (8 * i);
+        }
+        const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + ch * 8;
+        *reinterpret_cast<u32x4*>(y + off) = o;
+        if (idx) *reinterpret_cast<u32x2*>(idx + off) = u32x2{i0, i1};
+    }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx,
+                                                          bf16_t* __restrict__ dx, int N, int H, int W,
+                                                          int C, int OH, int OW, int k, int s, int p) {
+    const int cpr = C / 8;
+    const long total = (long)N * H * W * cpr;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int ch = t % cpr;
+        long pix = t / cpr;
+        const int iw = pix % W;
+        pix /= W;
+        const int ih = pix % H;
+        const int n = pix / H;
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(OH - 1, (ih + p) / s);
+        const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(OW - 1, (iw + p) / s);
+        for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+            const int dh = ih - (oh * s - p);
+            if (dh < 0 || dh >= k) continue;
+            for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+                const int dw = iw - (ow * s - p);
+                if (dw < 0 || dw >= k) continue;
+                const int want = dh * k + dw;
+                const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + ch * 8;
+                const u32x4 g = *reinterpret_cast<const u32x4*>(dy + off);
+                const u32x2 ii = *reinterpret_cast<const u32x2*>(idx + off);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t w = i < 2 ? ii[0] : ii[1];
+                    const int sh = 16 * (i & 1);
+                    if ((int)((w >> sh) & 0xff) == want) acc[2 * i] += lo_bf(g[i]);
+                    if ((int)((w >> (sh + 8)) & 0xff) == want) acc[2 * i + 1] += hi_bf(g[i]);
+                }
+            }
+        }
+        u32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = pack_bf2(acc[2 * i], acc[2 * i + 1]);
+        *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + ih) * W + iw) * C + ch * 8) = o;
+    }
+}
+
+// ------------------------------------------------------------------ avgpool
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y, int N, int HW, int C) {
+    const int cpr = C / 8;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * cpr) return;
+    const int n = t / cpr, ch = t % cpr;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16_t* p = x + (size_t)n * HW * C + ch * 8;
+    for (int i = 0; i < HW; ++i) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(p + (size_t)i * C);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc[2 * j] += lo_bf(w[j]);
+            acc[2 * j + 1] += hi_bf(w[j]);
+        }
+    }
+    const float inv = 1.f / (float)HW;
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf2(acc[2 * j] * inv, acc[2 * j + 1] * inv);
+    *reinterpret_cast<u32x4*>(y + (size_t)n * C + ch * 8) = o;
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          bf16_t* __restrict__ dx, int N, int HW, int C) {
+    const int cpr = C / 8;
+    const long total = (long)N * HW * cpr;
+    const float inv = 1.f / (float)HW;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int ch = t % cpr;
+        const long pix = t / cpr;
+        const int n = pix / HW;
+        const u32x4 g = *reinterpret_cast<const u32x4*>(dy + (size_t)n * C + ch * 8);
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf2(lo_bf(g[j]) * inv, hi_bf(g[j]) * inv);
+        *reinterpret_cast<u32x4*>(dx + pix * C + ch * 8) = o;
+    }
+}
+
+// ------------------------------------------------------- softmax xent + top-k
+// one wave per row. metrics[0] += loss, [1] += top1 hits, [2] += top5 hits, [3] += rows
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__ logits,
+                                                       const int64_t* __restrict__ labels,
+                                                       float* __restrict__ lse_out,
+                                                       float* __restrict__ loss_mean,
+                                                       float* __restrict__ metrics, int B, int NC,
+                                                       float smoothing) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    const float* z = logits + (size_t)row * NC;
+    const int64_t lab = labels[row];
+    float mx = -INFINITY;
+    for (int i = lane; i < NC; i += 64) mx = fmaxf(mx, z[i]);
+    mx = wave_max(mx);
+    float se = 0.f, sz = 0.f;
+    for (int i = lane; i < NC; i += 64) {
+        se += __expf(z[i] - mx);
+        sz += z[i];
+    }
+    se = wave_sum(se);
+    sz = wave_sum(sz);
+    const float lse = mx + __logf(se);
+    const float zl = (lab >= 0 && lab < NC) ? z[lab] : 0.f;
+    // rank of the label: #classes with a strictly larger logit
+    int gt = 0;
+    for (int i = lane; i < NC; i += 64) gt += z[i] > zl;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) gt += __shfl_xor(gt, o, 64);
+    if (lane == 0) {
+        const float nll = lse - zl;
+        const float loss = (1.f - smoothing) * nll + smoothing * (lse - sz / (float)NC);
+        lse_out[row] = lse;
+        atomicAdd(loss_mean, loss / (float)B);
+        if (metrics) {
+            atomicAdd(metrics + 0, loss);
+            atomicAdd(metrics + 1, gt < 1 ? 1.f : 0.f);
+            atomicAdd(metrics + 2, gt < 5 ? 1.f : 0.f);
+            atomicAdd(metrics + 3, 1.f);
+        }
+    }
+}
+
+// dlogits = g/B * (softmax - (1-eps)*onehot - eps/NC), bf16 out (feeds the fc dgrad/wgrad)
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const float* __restrict__ logits,
+                                                       const int64_t* __restrict__ labels,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ gout,
+                                                       bf16_t* __restrict__ dz, int B, int NC,
+                                                       float smoothing) {
+    const int row = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= NC) return;
+    const float scale = gout[0] / (float)B;
+    const float p = __expf(logits[(size_t)row * NC + i] - lse[row]);
+    const float t = (i == labels[row] ? 1.f - smoothing : 0.f) + smoothing / (float)NC;
+    dz[(size_t)row * NC + i] = f2bf((p - t) * scale);
+}
+
+__global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ x,
+                                                     float* __restrict__ out, int R, int C) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += bf2f(x[(size_t)r * C + c]);
+    out[c] += s;
+}
+
+// ------------------------------------------------------------------ SGD
+// torch.optim.SGD math ([torch] optim/sgd.py:343-380), on the flat arenas:
+//   g' = g*gs + wd*p ; buf = first ? g' : mu*buf + (1-damp)*g' ;
+//   d = nesterov ? g' + mu*buf : buf ; p -= lr*d ; shadow = bf16(p)
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ buf, bf16_t* __restrict__ shadow,
+                                                  long n, float lr, float mu, float damp, float wd,
+                                                  int nesterov, int first, float gs) {
+    const long n4 = n / 4;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4 + (n % 4 ? 1 : 0);
+         i += (long)gridDim.x * 256) {
+        if (i < n4) {
+            f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+            const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+            f32x4 bv = first ? f32x4{0, 0, 0, 0} : reinterpret_cast<f32x4*>(buf)[i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float gg = gv[j] * gs + wd * pv[j];
+                float b = mu != 0.f ? (first ? gg : mu * bv[j] + (1.f - damp) * gg) : gg;
+                bv[j] = b;
+                const float d = nesterov ? gg + mu * b : b;
+                pv[j] -= lr * d;
+            }
+            reinterpret_cast<f32x4*>(p)[i] = pv;
+            if (mu != 0.f) reinterpret_cast<f32x4*>(buf)[i] = bv;
+            if (shadow)
+                reinterpret_cast<u32x2*>(shadow)[i] = u32x2{pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3])};
+        } else {
+            for (long e = n4 * 4; e < n; ++e) {
+                float gg = g[e] * gs + wd * p[e];
+                float b = mu != 0.f ? (first ? gg : mu * buf[e] + (1.f - damp) * gg) : gg;
+                if (mu != 0.f) buf[e] = b;
+                const float d = nesterov ? gg + mu * b : b;
+                p[e] -= lr * d;
+                if (shadow) shadow[e] = f2bf(p[e]);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ p,
+                                                        bf16_t* __restrict__ o, long n) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) o[i] = f2bf(p[i]);
+}
+
+// --------------------------------------------------------- normalize (uint8)
+// in: uint8 [B][Hs][Ws][3] (decoded HWC images), out: bf16 [B][H][W][Cp]
+// out = (x/255 - mean)/std per channel, padded channels 0; per-sample crop
+// offset (oy, ox) and horizontal flip.
+__global__ __launch_bounds__(256) void normalize_kernel(const uint8_t* __restrict__ in,
+                                                        bf16_t* __restrict__ out,
+                                                        const int* __restrict__ crop,
+                                                        const uint8_t* __restrict__ flip, int B, int Hs,
+                                                        int Ws, int H, int W, int Cp, float m0, float m1,
+                                                        float m2, float is0, float is1, float is2) {
+    const long total = (long)B * H * W;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int w = t % W;
+        const long r = t / W;
+        const int h = r % H;
+        const int b = r / H;
+        const int oy = crop ? crop[2 * b] : 0, ox = crop ? crop[2 * b + 1] : 0;
+        const int sw = (flip && flip[b]) ? (W - 1 - w) : w;
+        const uint8_t* px = in + (((size_t)b * Hs + (h + oy)) * Ws + (sw + ox)) * 3;
+        const float c0 = ((float)px[0] * (1.f / 255.f) - m0) * is0;
+        const float c1 = ((float)px[1] * (1.f / 255.f) - m1) * is1;
+        const float c2 = ((float)px[2] * (1.f / 255.f) - m2) * is2;
+        bf16_t* o = out + (size_t)t * Cp;
+        if (Cp == 8) {
+            *reinterpret_cast<u32x4*>(o) = u32x4{pack_bf2(c0, c1), pack_bf2(c2, 0.f), 0u, 0u};
+        } else if (Cp == 4) {
+            *reinterpret_cast<u32x2*>(o) = u32x2{pack_bf2(c0, c1), pack_bf2(c2, 0.f)};
+        } else {
+            o[0] = f2bf(c0);
+            o[1] = f2bf(c1);
+            o[2] = f2bf(c2);
+            for (int c = 3; c < Cp; ++c) o[c] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------- batched weight transposes
+// dst[ci][t][co] = src[co][t][ci]  for every conv in the descriptor table.
+struct TDesc {
+    const bf16_t* src;
+    bf16_t* dst;
+    int Co, T, Ci;
+    int tile0;  // first global tile index of this descriptor
+};
+
+__global__ __launch_bounds__(256) void transpose_batched_kernel(const TDesc* __restrict__ d, int nd) {
+    __shared__ bf16_t tile[32][33];
+    int lo = 0, hi = nd - 1;
+    const int b = blockIdx.x;
+    while (lo < hi) {  // last descriptor with tile0 <= b
+        const int mid = (lo + hi + 1) >> 1;
+        if (d[mid].tile0 <= b) lo = mid; else hi = mid - 1;
+    }
+    const TDesc a = d[lo];
+    int rem = b - a.tile0;
+    const int nci = (a.Ci + 31) / 32, nco = (a.Co + 31) / 32;
+    const int tci = rem % nci;
+    rem /= nci;
+    const int tco = rem % nco;
+    const int t = rem / nco;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int r = ty; r < 32; r += 8) {
+        const int co = tco * 32 + r, ci = tci * 32 + tx;
+        if (co < a.Co && ci < a.Ci) tile[r][tx] = a.src[((size_t)co * a.T + t) * a.Ci + ci];
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int ci = tci * 32 + r, co = tco * 32 + tx;
+        if (co < a.Co && ci < a.Ci) a.dst[((size_t)ci * a.T + t) * a.Co + co] = tile[tx][r];
+    }
+}
+
+int stream_grid(long work, int per_block = 256) {
+    long b = (work + per_block - 1) / per_block;
+    return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+IMK_EXPORT int imk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH,
+                               int OW, int k, int s, int p, void* stream) {
+    if (C % 8) return -100;
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid((long)N * OH * OW * (C / 8))), dim3(256),
+                       0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, N, H, W, C,
+                       OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C,
+                               int OH, int OW, int k, int s, int p, void* stream) {
+    if (C % 8) return -100;
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid((long)N * H * W * (C / 8))), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, H,
+                       W, C, OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_avgpool_fwd(const void* x, void* y, int N, int HW, int C, void* stream) {
+    if (C % 8) return -100;
+    const int threads = N * (C / 8);
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((threads + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, N, HW, C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, void* stream) {
+    if (C % 8) return -100;
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(stream_grid((long)N * HW * (C / 8))), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, N, HW, C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_xent_fwd(const float* logits, const int64_t* labels, float* lse, float* loss_mean,
+                            float* metrics, int B, int NC, float smoothing, void* stream) {
+    hipLaunchKernelGGL(xent_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits,
+                       labels, lse, loss_mean, metrics, B, NC, smoothing);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_xent_bwd(const float* logits, const int64_t* labels, const float* lse,
+                            const float* gout, void* dz, int B, int NC, float smoothing, void* stream) {
+    hipLaunchKernelGGL(xent_bwd_kernel, dim3((NC + 255) / 256, B), dim3(256), 0, (hipStream_t)stream,
+                       logits, labels, lse, gout, (bf16_t*)dz, B, NC, smoothing);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_colsum_bf16(const void* x, float* out, int R, int C, void* stream) {
+    hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, out, R, C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_sgd(float* p, const float* g, float* buf, void* shadow, long n, float lr, float mu,
+                       float damp, float wd, int nesterov, int first, float gs, void* stream) {
+    hipLaunchKernelGGL(sgd_kernel, dim3(stream_grid((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, p,
+                       g, buf, (bf16_t*)shadow, n, lr, mu, damp, wd, nesterov, first, gs);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_cast_bf16(const float* p, void* o, long n, void* stream) {
+    hipLaunchKernelGGL(cast_bf16_kernel, dim3(stream_grid(n)), dim3(256), 0, (hipStream_t)stream, p,
+                       (bf16_t*)o, n);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_normalize_u8(const void* in, void* out, const int* crop, const void* flip, int B,
+                                int Hs, int Ws, int H, int W, int Cp, const float* mean,
+                                const float* std, void* stream) {
+    hipLaunchKernelGGL(normalize_kernel, dim3(stream_grid((long)B * H * W)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint8_t*)in, (bf16_t*)out, crop,
+                       (const uint8_t*)flip, B, Hs, Ws, H, W, Cp, mean[0], mean[1], mean[2],
+                       1.f / std[0], 1.f / std[1], 1.f / std[2]);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_transpose_batched(const void* descs, int nd, int total_tiles, void* stream) {
+    if (nd <= 0) return 0;
+    hipLaunchKernelGGL(transpose_batched_kernel, dim3(total_tiles), dim3(256), 0, (hipStream_t)stream,
+                       (const TDesc*)descs, nd);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_tdesc_size() { return (int)sizeof(TDesc); }

@@ -1,0 +1,203 @@
+"""Binding of a ResNet to the MI355X kernel path and its NHWC forward.
+
+``bind_native(model, device, order)`` re-homes the parameters into a
+:class:`ParamArena` (fp32 master + grad + bf16 shadow, bucket order), builds
+the dgrad weight shadows (batched transpose plan), the padded stem weight
+(3 -> 8 input channels for 16-B NHWC loads) and one device workspace arena
+for every BatchNorm (conv-epilogue statistics, saved mean/invstd, backward
+scratch) that is zeroed with a single memset per training step.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import torch
+
+from ..ops import _lib
+from ..ops.bn import BNActFn, bn_eval, running_update
+from ..ops.conv import ConvFn, LinearFn, igemm_fwd
+from ..ops.misc import AvgPoolFn, MaxPoolFn, TransposePlan, maxpool_eval
+from .arena import ParamArena
+from .resnet import BasicBlock, BatchNorm2d, BNWork, Bottleneck, Conv2d, Linear, ResNet
+
+
+class NativeState:
+    def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None):
+        self.device = torch.device(device)
+        named = list(model.named_parameters())
+        self.arena = ParamArena(named, self.device, order=order, with_shadow=True)
+        self.model = model
+        self._bind_shadows()
+        self._bind_workspace()
+
+    # ------------------------------------------------------------ shadows
+    def _bind_shadows(self):
+        m, ar = self.model, self.arena
+        dev = self.device
+        st_items = []
+        t_numel = 0
+        convs: List[Conv2d] = m.convs()
+        for c in convs:
+            sh = ar.shadow(c.weight).view(c.out_channels, c.kh, c.kw, c.in_channels)
+            c.w_bf16 = sh
+            c.grad_pad = None
+            if c is not m.conv1:
+                t_numel += sh.numel()
+        fc: Linear = m.fc
+        fc.w_bf16 = ar.shadow(fc.weight).view(fc.out_features, fc.in_features)
+        t_numel += fc.w_bf16.numel()
+        self.T = torch.empty(t_numel, dtype=torch.bfloat16, device=dev)
+        off = 0
+        for c in convs:
+            if c is m.conv1:
+                continue
+            n = c.w_bf16.numel()
+            c.wt_bf16 = self.T[off:off + n].view(c.in_channels, c.kh, c.kw, c.out_channels)
+            st_items.append((c.w_bf16, c.wt_bf16, c.out_channels, c.kh * c.kw, c.in_channels))
+            off += n
+        n = fc.w_bf16.numel()
+        fc.wt_bf16 = self.T[off:off + n].view(fc.in_features, fc.out_features)
+        st_items.append((fc.w_bf16, fc.wt_bf16, fc.out_features, 1, fc.in_features))
+        self.tplan = TransposePlan(st_items, dev)
+        # stem: pad Ci 3 -> 8
+        s = m.conv1
+        cp = ResNet.STEM_CPAD
+        s.w_pad = torch.zeros((s.out_channels, s.kh, s.kw, cp), dtype=torch.bfloat16, device=dev)
+        s.grad_pad = torch.zeros((s.out_channels, s.kh, s.kw, cp), dtype=torch.float32, device=dev)
+        s.w_bf16_real = s.w_bf16
+        s.w_bf16 = s.w_pad
+
+    def refresh_shadows(self, full: bool = False) -> None:
+        """Bring the bf16 copies in line with the fp32 masters. ``full`` also
+        re-casts the masters (after init / checkpoint load); the optimizer
+        step already writes ``S`` itself."""
+        from ..ops.misc import cast_bf16
+        if full:
+            cast_bf16(self.arena.P, self.arena.S)
+        self.tplan.run()
+        s = self.model.conv1
+        s.w_pad[..., : s.in_channels].copy_(s.w_bf16_real)
+
+    # ---------------------------------------------------------- workspace
+    def _bind_workspace(self):
+        bns: List[BatchNorm2d] = self.model.batchnorms()
+        sizes = [bn.num_features for bn in bns]
+        per = [2 * c + 3 * c for c in sizes]           # stats + scratch (zeroed)
+        self.zero_ws = torch.zeros(sum(per), dtype=torch.float32, device=self.device)
+        self.save_ws = torch.zeros(sum(2 * c for c in sizes), dtype=torch.float32, device=self.device)
+        o = so = 0
+        descs = (_lib.RunDesc * len(bns))()
+        for i, bn in enumerate(bns):
+            c = bn.num_features
+            stats = self.zero_ws[o:o + 2 * c]
+            scratch = self.zero_ws[o + 2 * c:o + 5 * c]
+            save = self.save_ws[so:so + 2 * c]
+            bn.work = BNWork(stats, None, save, None, scratch)
+            o += 5 * c
+            so += 2 * c
+            d = descs[i]
+            d.sums, d.rmean, d.rvar = stats.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+            d.nbt = bn.num_batches_tracked.data_ptr()
+            d.C = c
+            d.momentum = bn.momentum
+        self._run_descs = descs
+        self.bns = bns
+
+    def running_update(self, rows: List[int]) -> None:
+        """After a training forward: update every BN's running stats in one launch."""
+        key = tuple(rows)
+        if getattr(self, "_run_key", None) != key:
+            for d, r in zip(self._run_descs, rows):
+                d.inv_cnt = 1.0 / r
+                d.unbias = r / max(1, r - 1)
+            raw = bytes(memoryview(self._run_descs))
+            self._run_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+            self._run_key = key
+        running_update(self._run_dev, len(self.bns))
+
+
+def bind_native(model: ResNet, device, order: Optional[Sequence[int]] = None) -> NativeState:
+    model.to(device)
+    st = NativeState(model, device, order)
+    model.native = st
+    model.backend = "hip"
+    st.refresh_shadows(full=True)
+    return st
+
+
+# --------------------------------------------------------------------------
+# forward
+# --------------------------------------------------------------------------
+
+def _conv(x, conv: Conv2d, bn: Optional[BatchNorm2d], train: bool):
+    if train:
+        return ConvFn.apply(x, conv.weight, conv, bn.work.stats if bn is not None else None)
+    return igemm_fwd(x, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw)
+
+
+def _bn(x, bn, relu, train, x2=None, bn2=None, mode=0):
+    if train:
+        return BNActFn.apply(x, x2, bn, bn2, mode, relu)
+    return bn_eval(x, bn, relu, x2=x2, bn2=bn2, mode=mode)
+
+
+def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
+    """x: NHWC bf16 [N, H, W, 8] (normalised, channels 3..7 zero) -> fp32 logits."""
+    st: NativeState = model.native
+    if x.dtype != torch.bfloat16 or x.dim() != 4 or x.shape[-1] != ResNet.STEM_CPAD:
+        raise ValueError(f"hip backend expects NHWC bf16 [N,H,W,{ResNet.STEM_CPAD}], got "
+                         f"{tuple(x.shape)} {x.dtype}")
+    train = model.training and torch.is_grad_enabled()
+    if train:
+        st.zero_ws.zero_()
+    rows = []
+    y = _conv(x, model.conv1, model.bn1, train)
+    rows.append(y.numel() // y.shape[-1])
+    y = _bn(y, model.bn1, True, train)
+    y = MaxPoolFn.apply(y, 3, 2, 1) if train else maxpool_eval(y, 3, 2, 1)
+    for b in model.blocks():
+        idt = y
+        pairs = b.convs_bns()
+        out = y
+        for conv, bn, relu in pairs[:-1]:
+            a = _conv(out, conv, bn, train)
+            rows.append(a.numel() // a.shape[-1])
+            out = _bn(a, bn, True, train)
+        conv, bn, _ = pairs[-1]
+        a = _conv(out, conv, bn, train)
+        rows.append(a.numel() // a.shape[-1])
+        if b.downsample is not None:
+            dconv, dbn = b.downsample[0], b.downsample[1]
+            ad = _conv(idt, dconv, dbn, train)
+            rows.append(ad.numel() // ad.shape[-1])
+            y = _bn(a, bn, True, train, x2=ad, bn2=dbn, mode=2)
+        else:
+            y = _bn(a, bn, True, train, x2=idt, mode=1)
+    pooled = AvgPoolFn.apply(y) if train else _avg_eval(y)
+    if train:
+        logits = LinearFn.apply(pooled, model.fc.weight, model.fc)
+        st.running_update(_rows_in_bn_order(model, rows))
+    else:
+        fc = model.fc
+        B = pooled.shape[0]
+        logits = igemm_fwd(pooled.view(B, 1, 1, -1), fc.w_bf16.view(fc.out_features, 1, 1, -1), 1, 0, 1,
+                           1, bias=fc.bias, out_f32=True).view(B, -1)
+    return logits
+
+
+def _avg_eval(y):
+    from ..ops.misc import _lib as L
+    N, H, W, Cc = y.shape
+    out = torch.empty((N, Cc), device=y.device, dtype=y.dtype)
+    L.check(L.kernels().imk_avgpool_fwd(y.data_ptr(), out.data_ptr(), N, H * W, Cc, L.stream_ptr()),
+            "avgpool")
+    return out
+
+
+def _rows_in_bn_order(model: ResNet, rows_fwd: List[int]) -> List[int]:
+    """Map the per-conv row counts (forward order) onto model.batchnorms() order."""
+    # forward order: stem, then per block conv1..convK, [downsample]; batchnorms()
+    # (module order) lists: bn1, then per block bn1..bnK, [downsample.1] -> identical.
+    return rows_fwd

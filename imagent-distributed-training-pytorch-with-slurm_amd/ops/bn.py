@@ -1,0 +1,96 @@
+"""BatchNorm(+residual add)(+ReLU) on the fused HIP kernels (NHWC bf16).
+
+Training-mode statistics arrive from the producing conv's epilogue as
+per-channel (sum, sum of squares) in fp32 (``stats``), so the forward is one
+streaming pass. ``save`` receives (mean, invstd) for the backward.
+
+Three forms cover torchvision's blocks (reference model: ``imagenet.py:312``):
+  mode 0  y = act(bn(x))                       (conv1/conv2 of a block, stem)
+  mode 1  y = act(bn(x) + res)                 (last BN of a block, identity shortcut)
+  mode 2  y = act(bn(x) + bn_d(x2))            (last BN + downsample BN, fused)
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .grad_sink import notify_ready
+
+
+def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
+                  save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False):
+    C = x.shape[-1]
+    R = x.numel() // C
+    _lib.check(_lib.kernels().imk_bn_fwd(
+        x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _lib.ptr(x2),
+        _lib.ptr(stats2), _lib.ptr(gamma2), _lib.ptr(beta2), y.data_ptr(), _lib.ptr(save),
+        _lib.ptr(save2), R, C, mode, 1 if relu else 0, eps, 1 if eval_mode else 0,
+        _lib.stream_ptr()), "bn fwd")
+
+
+class BNActFn(torch.autograd.Function):
+    """y = act(bn(x) [+ res | + bn2(x2)]); gamma/beta grads go to the arena.
+
+    ``bn.work`` holds the conv-epilogue statistics (``stats``), the saved
+    (mean, invstd) (``save``) and the zeroed backward scratch."""
+
+    @staticmethod
+    def forward(ctx, x, x2, bn, bn2, mode, relu):
+        y = torch.empty_like(x)
+        w, w2 = bn.work, (bn2.work if bn2 is not None else None)
+        bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
+                      stats2=w2.stats if w2 is not None else None,
+                      gamma2=bn2.weight if bn2 is not None else None,
+                      beta2=bn2.bias if bn2 is not None else None,
+                      save2=w2.save if w2 is not None else None, mode=mode, relu=relu, eps=bn.eps)
+        ctx.bn, ctx.bn2, ctx.mode, ctx.relu = bn, bn2, mode, relu
+        ctx.save_for_backward(x, x2 if mode == 2 else None, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2, y = ctx.saved_tensors
+        bn, bn2, mode = ctx.bn, ctx.bn2, ctx.mode
+        w = bn.work
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        R = x.numel() // C
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if mode == 1 else None
+        dx2 = torch.empty_like(x2) if mode == 2 else None
+        _lib.check(_lib.kernels().imk_bn_bwd(
+            dy.data_ptr(), y.data_ptr() if ctx.relu else 0, x.data_ptr(), w.save.data_ptr(),
+            bn.weight.data_ptr(), _lib.ptr(x2) if mode == 2 else 0,
+            bn2.work.save.data_ptr() if mode == 2 else 0,
+            bn2.weight.data_ptr() if mode == 2 else 0, w.scratch.data_ptr(), dx.data_ptr(),
+            _lib.ptr(dres), _lib.ptr(dx2), bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
+            bn2.weight.grad.data_ptr() if mode == 2 else 0,
+            bn2.bias.grad.data_ptr() if mode == 2 else 0,
+            R, C, mode, 1 if ctx.relu else 0, _lib.stream_ptr()), "bn bwd")
+        notify_ready(bn.weight)
+        notify_ready(bn.bias)
+        if mode == 2:
+            notify_ready(bn2.weight)
+            notify_ready(bn2.bias)
+        return dx, (dres if mode == 1 else dx2), None, None, None, None
+
+
+def bn_eval(x, bn, relu, x2=None, bn2=None, mode=0):
+    """Inference BN (running statistics), same fusions, no autograd."""
+    y = torch.empty_like(x)
+    rs = torch.stack([bn.running_mean, bn.running_var])
+    rs2 = torch.stack([bn2.running_mean, bn2.running_var]) if bn2 is not None else None
+    bn_fwd_launch(x, rs, bn.weight, bn.bias, y, None, x2=x2, stats2=rs2,
+                  gamma2=bn2.weight if bn2 is not None else None,
+                  beta2=bn2.bias if bn2 is not None else None, mode=mode, relu=relu, eps=bn.eps,
+                  eval_mode=True)
+    return y
+
+
+def running_update(desc_tensor: torch.Tensor, n: int) -> None:
+    """One launch updates running_mean/var and num_batches_tracked of every BN."""
+    _lib.check(_lib.kernels().imk_bn_running_update(desc_tensor.data_ptr(), n, _lib.stream_ptr()),
+               "bn running update")

@@ -1,0 +1,195 @@
+"""Convolution / linear on the hand-written MFMA implicit-GEMM kernels.
+
+Activations are NHWC bf16 tensors ``[N, H, W, C]``; weights are the fp32
+master parameters (torchvision shape ``[Co, Ci, KH, KW]`` stored
+channels-last, i.e. ``[Co][KH][KW][Ci]`` in memory) plus two bf16 shadows kept
+current by the optimizer step: ``w`` ``[Co][KH][KW][Ci]`` for the forward and
+wgrad, ``wt`` ``[Ci][KH][KW][Co]`` for the dgrad.
+
+Reference counterpart: the cuDNN convolutions torchvision's resnet issues
+(``/root/reference/imagenet.py:312`` model, fwd ``:123``, bwd ``:128``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from .grad_sink import notify_ready
+
+
+def conv_out_size(h: int, k: int, s: int, p: int) -> int:
+    return (h + 2 * p - k) // s + 1
+
+
+def _magic(d: int) -> Tuple[int, int]:
+    """Unsigned magic-number division constants: q = (umulhi(n, m) + n) >> s."""
+    if d <= 1:
+        return 0, 0
+    s = (d - 1).bit_length()
+    m = ((1 << 32) * ((1 << s) - d)) // d + 1
+    return m & 0xFFFFFFFF, s
+
+
+def _base_args(x_ptr, w_ptr, y_ptr, N, H, W, Cin, OH, OW, Nout, ldb, sA) -> _lib.IGemmArgs:
+    a = _lib.IGemmArgs()
+    a.X, a.Wk, a.Y = x_ptr, w_ptr, y_ptr
+    a.bias = None
+    a.stats = None
+    a.N, a.H, a.W, a.C = N, H, W, Cin
+    a.OH, a.OW, a.M = OH, OW, N * OH * OW
+    a.Nout, a.ldb, a.sA = Nout, ldb, sA
+    return a
+
+
+def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
+              stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+              out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
+              tile: int = 0) -> torch.Tensor:
+    """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
+    per-channel (sum, sumsq) accumulation into ``stats`` [2, Co]."""
+    N, H, W, Ci = x.shape
+    Co = w.shape[0]
+    OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
+    if out is None:
+        out = torch.empty((N, OH, OW, Co), device=x.device,
+                          dtype=torch.float32 if out_f32 else torch.bfloat16)
+    a = _base_args(x.data_ptr(), w.data_ptr(), out.data_ptr(), N, H, W, Ci, OH, OW, Co, KH * KW * Ci,
+                   stride)
+    a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = KH, KW, -pad, 1, -pad, 1
+    a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
+    a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
+    a.flags = (1 if out_f32 else 0) | (2 if relu else 0)
+    if bias is not None:
+        a.bias = bias.data_ptr()
+    if stats is not None:
+        a.stats = stats.data_ptr()
+    _lib.check(_lib.kernels().imk_conv_igemm(C.byref(a), tile, _lib.stream_ptr()), "conv fwd")
+    return out
+
+
+def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
+                KH: int, KW: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx[N,H,W,Ci] from dy[N,OH,OW,Co] and wt[Ci,KH,KW,Co].
+
+    Stride 1: one gather-GEMM launch with the taps mirrored.
+    Stride s: s*s launches, one per output parity class, each touching only
+    the taps that hit it (sub-pixel decomposition: no multiply-by-zero work).
+    """
+    N, OH, OW, Co = dy.shape
+    Ci = wt.shape[0]
+    H, W = in_hw
+    if out is None:
+        out = torch.empty((N, H, W, Ci), device=dy.device, dtype=torch.bfloat16)
+    k = _lib.kernels()
+    st = _lib.stream_ptr()
+    S = stride
+    for ph in range(S):
+        for pw in range(S):
+            gh = (H - ph + S - 1) // S  # rows of this parity class
+            gw = (W - pw + S - 1) // S
+            if gh <= 0 or gw <= 0:
+                continue
+            kh0 = (ph + pad) % S
+            kw0 = (pw + pad) % S
+            nth = max(0, (KH - kh0 + S - 1) // S)
+            ntw = max(0, (KW - kw0 + S - 1) // S)
+            a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
+                           KH * KW * Co, 1)
+            a.nth, a.ntw = nth, ntw
+            a.dh0, a.dhs = (ph + pad - kh0) // S, -1
+            a.dw0, a.dws = (pw + pad - kw0) // S, -1
+            a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
+            a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
+            a.flags = 0
+            _lib.check(k.imk_conv_igemm(C.byref(a), 0, st), "conv dgrad")
+    return out
+
+
+def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int, KH: int,
+                KW: int, splits: int = 0) -> None:
+    """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci])."""
+    N, H, W, Ci = x.shape
+    _, OH, OW, Co = dy.shape
+    a = _lib.WgradArgs()
+    a.dY, a.X, a.dW = dy.data_ptr(), x.data_ptr(), dw.data_ptr()
+    a.N, a.H, a.W, a.Ci, a.Co = N, H, W, Ci, Co
+    a.OH, a.OW, a.M = OH, OW, N * OH * OW
+    a.KH, a.KW, a.stride, a.pad = KH, KW, stride, pad
+    a.m_per_split = 0
+    a.mg_ohw, a.sh_ohw = _magic(OH * OW)
+    a.mg_ow, a.sh_ow = _magic(OW)
+    _lib.check(_lib.kernels().imk_conv_wgrad(C.byref(a), splits, _lib.stream_ptr()), "conv wgrad")
+
+
+def colsum_into(x2d: torch.Tensor, out: torch.Tensor) -> None:
+    R, Cc = x2d.shape
+    _lib.check(_lib.kernels().imk_colsum_bf16(x2d.data_ptr(), out.data_ptr(), R, Cc, _lib.stream_ptr()),
+               "colsum")
+
+
+# --------------------------------------------------------------------------
+# autograd
+# --------------------------------------------------------------------------
+
+class ConvFn(torch.autograd.Function):
+    """NHWC bf16 conv whose weight gradient lands directly in the parameter's
+    slot of the flat fp32 gradient arena (``weight.grad``), then signals the
+    bucketed reducer. ``weight`` is passed only to anchor the node in the
+    graph (the stem conv's input needs no grad); autograd never sees dW."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mod, stats):
+        y = igemm_fwd(x, mod.w_bf16, mod.stride, mod.padding, mod.kh, mod.kw, stats=stats)
+        ctx.mod = mod
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        mod = ctx.mod
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = igemm_dgrad(dy, mod.wt_bf16, (x.shape[1], x.shape[2]), mod.stride, mod.padding, mod.kh,
+                             mod.kw)
+        gp = getattr(mod, "grad_pad", None)
+        if gp is not None:  # stem: input channels padded 3 -> 8 for 16-B NHWC loads
+            gp.zero_()
+            igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw)
+            mod.weight.grad.permute(0, 2, 3, 1).add_(gp[..., : mod.in_channels])
+        else:
+            igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw)
+        notify_ready(mod.weight)
+        return dx, None, None, None
+
+
+class LinearFn(torch.autograd.Function):
+    """fc layer as a 1x1 conv on a 1x1 image: x [B, Cin] bf16 -> logits fp32 [B, Cout]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mod):
+        B, Cin = x.shape
+        y = igemm_fwd(x.view(B, 1, 1, Cin), mod.w_bf16.view(mod.out_features, 1, 1, Cin), 1, 0, 1, 1,
+                      bias=mod.bias, out_f32=True)
+        ctx.mod = mod
+        ctx.save_for_backward(x)
+        return y.view(B, -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        mod = ctx.mod
+        B, Cin = x.shape
+        dyb = dy.to(torch.bfloat16).contiguous().view(B, 1, 1, -1)
+        dx = igemm_dgrad(dyb, mod.wt_bf16.view(Cin, 1, 1, -1), (1, 1), 1, 0, 1, 1).view(B, Cin)
+        igemm_wgrad(dyb, x.view(B, 1, 1, Cin), mod.weight.grad, 1, 0, 1, 1)
+        notify_ready(mod.weight)
+        if mod.bias is not None:
+            colsum_into(dyb.view(B, -1), mod.bias.grad)
+            notify_ready(mod.bias)
+        return dx, None, None

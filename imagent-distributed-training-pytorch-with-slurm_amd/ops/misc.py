@@ -1,0 +1,154 @@
+"""Pooling, loss + metrics, optimizer and input kernels (Python side)."""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from .conv import conv_out_size
+
+
+# ----------------------------------------------------------------- pooling
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        N, H, W, Cc = x.shape
+        OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
+        y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
+        idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
+        _lib.check(_lib.kernels().imk_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W,
+                                                  Cc, OH, OW, k, s, p, _lib.stream_ptr()), "maxpool")
+        ctx.save_for_backward(idx)
+        ctx.geom = (N, H, W, Cc, OH, OW, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, H, W, Cc, OH, OW, k, s, p = ctx.geom
+        dx = torch.empty((N, H, W, Cc), device=dy.device, dtype=torch.bfloat16)
+        _lib.check(_lib.kernels().imk_maxpool_bwd(dy.contiguous().data_ptr(), idx.data_ptr(),
+                                                  dx.data_ptr(), N, H, W, Cc, OH, OW, k, s, p,
+                                                  _lib.stream_ptr()), "maxpool bwd")
+        return dx, None, None, None
+
+
+def maxpool_eval(x, k, s, p):
+    N, H, W, Cc = x.shape
+    OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
+    y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
+    _lib.check(_lib.kernels().imk_maxpool_fwd(x.data_ptr(), y.data_ptr(), None, N, H, W, Cc, OH, OW,
+                                              k, s, p, _lib.stream_ptr()), "maxpool")
+    return y
+
+
+class AvgPoolFn(torch.autograd.Function):
+    """Global average pool NHWC [N,H,W,C] -> [N,C] (AdaptiveAvgPool2d((1,1)) + flatten)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, Cc = x.shape
+        y = torch.empty((N, Cc), device=x.device, dtype=x.dtype)
+        _lib.check(_lib.kernels().imk_avgpool_fwd(x.data_ptr(), y.data_ptr(), N, H * W, Cc,
+                                                  _lib.stream_ptr()), "avgpool")
+        ctx.shape = (N, H, W, Cc)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, Cc = ctx.shape
+        dx = torch.empty((N, H, W, Cc), device=dy.device, dtype=torch.bfloat16)
+        _lib.check(_lib.kernels().imk_avgpool_bwd(dy.to(torch.bfloat16).contiguous().data_ptr(),
+                                                  dx.data_ptr(), N, H * W, Cc, _lib.stream_ptr()),
+                   "avgpool bwd")
+        return dx
+
+
+# ------------------------------------------------------------ loss+metrics
+class XentFn(torch.autograd.Function):
+    """Mean softmax cross-entropy (nn.CrossEntropyLoss, imagenet.py:323) with
+    fused top-1/top-5 counting into a device metrics vector
+    ``[loss_sum, top1_hits, top5_hits, rows]`` - no host sync per step."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, metrics, smoothing):
+        logits = logits.contiguous()
+        B, NC = logits.shape
+        lse = torch.empty(B, device=logits.device, dtype=torch.float32)
+        loss = torch.zeros((), device=logits.device, dtype=torch.float32)
+        _lib.check(_lib.kernels().imk_xent_fwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(),
+                                               loss.data_ptr(), _lib.ptr(metrics), B, NC,
+                                               float(smoothing), _lib.stream_ptr()), "xent")
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.smoothing = smoothing
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, labels, lse = ctx.saved_tensors
+        B, NC = logits.shape
+        dz = torch.empty((B, NC), device=logits.device, dtype=torch.bfloat16)
+        g = gout.to(torch.float32).contiguous()
+        _lib.check(_lib.kernels().imk_xent_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(),
+                                               g.data_ptr(), dz.data_ptr(), B, NC,
+                                               float(ctx.smoothing), _lib.stream_ptr()), "xent bwd")
+        return dz, None, None, None
+
+
+# -------------------------------------------------------------------- SGD
+def sgd_flat(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor],
+             shadow: Optional[torch.Tensor], lr: float, momentum: float, dampening: float,
+             weight_decay: float, nesterov: bool, first: bool, grad_scale: float = 1.0) -> None:
+    _lib.check(_lib.kernels().imk_sgd(p.data_ptr(), g.data_ptr(), _lib.ptr(buf), _lib.ptr(shadow),
+                                      p.numel(), lr, momentum, dampening, weight_decay,
+                                      1 if nesterov else 0, 1 if first else 0, grad_scale,
+                                      _lib.stream_ptr()), "sgd")
+
+
+def cast_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
+    _lib.check(_lib.kernels().imk_cast_bf16(src.data_ptr(), dst.data_ptr(), src.numel(),
+                                            _lib.stream_ptr()), "cast")
+
+
+class TransposePlan:
+    """Batched ``[Co][T][Ci] -> [Ci][T][Co]`` re-layout of every conv's bf16
+    weight shadow into its dgrad shadow: one launch per optimizer step."""
+
+    def __init__(self, items: Sequence[tuple], device):
+        descs = (_lib.TDesc * max(1, len(items)))()
+        tile = 0
+        for i, (src, dst, Co, T, Ci) in enumerate(items):
+            descs[i].src, descs[i].dst = src.data_ptr(), dst.data_ptr()
+            descs[i].Co, descs[i].T, descs[i].Ci, descs[i].tile0 = Co, T, Ci, tile
+            tile += ((Co + 31) // 32) * ((Ci + 31) // 32) * T
+        raw = bytes(memoryview(descs))[: C.sizeof(_lib.TDesc) * len(items)]
+        self.n = len(items)
+        self.tiles = tile
+        self.desc = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device) if items else None
+
+    def run(self) -> None:
+        if self.n:
+            _lib.check(_lib.kernels().imk_transpose_batched(self.desc.data_ptr(), self.n, self.tiles,
+                                                            _lib.stream_ptr()), "transpose")
+
+
+# -------------------------------------------------------------- normalize
+def normalize_u8(images: torch.Tensor, out_hw, cpad: int, mean: Sequence[float], std: Sequence[float],
+                 crop: Optional[torch.Tensor] = None, flip: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [B, Hs, Ws, 3] -> bf16 NHWC [B, H, W, cpad]: (x/255 - mean)/std
+    (ToTensor + Normalize of imagenet.py:280-283, on the GPU)."""
+    B, Hs, Ws, _ = images.shape
+    H, W = out_hw
+    if out is None:
+        out = torch.empty((B, H, W, cpad), device=images.device, dtype=torch.bfloat16)
+    m = (C.c_float * 3)(*mean)
+    s = (C.c_float * 3)(*std)
+    _lib.check(_lib.kernels().imk_normalize_u8(images.data_ptr(), out.data_ptr(), _lib.ptr(crop),
+                                               _lib.ptr(flip), B, Hs, Ws, H, W, cpad,
+                                               C.cast(m, C.c_void_p), C.cast(s, C.c_void_p),
+                                               _lib.stream_ptr()), "normalize")
+    return out

@@ -1,0 +1,293 @@
+"""Bucketed data parallelism over the flat gradient arena.
+
+Capabilities of ``DistributedDataParallel(model, device_ids=[local_rank])``
+as the reference uses it (``imagenet.py:316``):
+
+* init: parameter-shape verification across ranks + broadcast of parameters
+  and buffers from rank 0 ([torch] distributed.py:862-864);
+* backward: gradients are averaged across ranks by bucketed all-reduces that
+  start while the rest of the backward is still running;
+* iteration 1 observes the real gradient-ready order and the buckets are
+  rebuilt once from it ([torch] distributed.py:1551);
+* BatchNorm buffers: the reference broadcasts them from rank 0 before EVERY
+  forward (``broadcast_buffers=True``). Default here is ``'eval'``: broadcast
+  only before validation / checkpointing (the per-step 40-tensor latency-bound
+  broadcast buys nothing for per-GPU BN statistics); ``'always'`` restores
+  the reference's behaviour exactly.
+
+MI355X design:
+* the gradients ARE the buckets (contiguous slices of the arena, in bucket
+  order) - the native wgrad / BN-backward kernels accumulate straight into
+  them and call :func:`~imagent_amd.ops.grad_sink.notify_ready`;
+* bookkeeping (bucket plan, ready tracking, in-order launch) is the C++
+  runtime (``csrc/runtime/reducer.cpp``);
+* each complete bucket is all-reduced (``ncclAvg``) on the communicator's
+  high-priority side stream, ordered after the producing kernels by an event;
+  the compute stream joins once at the end of backward. Bucket sizes target
+  xGMI: a small first bucket (fc grads are ready first) and mid-size caps
+  so several collectives overlap the remaining backward.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import ctypes as C
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..models.arena import ParamArena
+from ..ops import _lib
+from .comm import Communicator, LocalCommunicator
+
+MB = 1024 * 1024
+
+
+def plan_buckets(nbytes: List[int], first_cap: int, cap: int) -> List[int]:
+    """Bucket id per tensor (tensors given in bucket/layout order)."""
+    n = len(nbytes)
+    if n == 0:
+        return []
+    try:
+        L = _lib.runtime()
+        arr = (C.c_int64 * n)(*nbytes)
+        out = (C.c_int32 * n)()
+        L.imr_plan_buckets(n, arr, first_cap, cap, out)
+        return list(out)
+    except _lib.NativeLibraryMissing:
+        ids, b, acc, lim = [], 0, 0, first_cap if first_cap > 0 else cap
+        for i, s in enumerate(nbytes):
+            ids.append(b)
+            acc += s
+            if acc >= lim and i + 1 < n:
+                b, acc, lim = b + 1, 0, cap
+        return ids
+
+
+class _Tracker:
+    """ctypes wrapper of the native ready tracker (pure-Python fallback)."""
+
+    def __init__(self, bucket_of: List[int], nbuckets: int):
+        self.n, self.nb = len(bucket_of), nbuckets
+        try:
+            self.L = _lib.runtime()
+            arr = (C.c_int32 * self.n)(*bucket_of)
+            self.h = self.L.imr_tracker_new(self.n, arr, nbuckets)
+            self._first, self._count = C.c_int32(), C.c_int32()
+        except _lib.NativeLibraryMissing:
+            self.L = None
+            self.bucket_of = list(bucket_of)
+            self.size = [0] * nbuckets
+            for b in bucket_of:
+                self.size[b] += 1
+            self._reset()
+
+    def _reset(self):
+        self.pending = list(self.size)
+        self.marked = [False] * self.n
+        self.next = 0
+        self.order: List[int] = []
+
+    def mark(self, i: int):
+        if self.L is not None:
+            rc = self.L.imr_tracker_mark(self.h, i, C.byref(self._first), C.byref(self._count))
+            if rc == -1:
+                raise RuntimeError(f"parameter {i} marked ready twice in one iteration (used twice "
+                                   "in the forward?)")
+            if rc != 0:
+                raise RuntimeError(f"tracker error {rc}")
+            return self._first.value, self._count.value
+        if self.marked[i]:
+            raise RuntimeError(f"parameter {i} marked ready twice in one iteration")
+        self.marked[i] = True
+        self.order.append(i)
+        self.pending[self.bucket_of[i]] -= 1
+        first = self.next
+        while self.next < self.nb and self.pending[self.next] == 0:
+            self.next += 1
+        return first, self.next - first
+
+    def finalize(self):
+        if self.L is not None:
+            unready = (C.c_uint8 * self.n)()
+            missing = self.L.imr_tracker_finalize(self.h, unready)
+            order = (C.c_int32 * self.n)()
+            k = self.L.imr_tracker_last_order(self.h, order)
+            return missing, [i for i in range(self.n) if unready[i]], list(order)[:k]
+        missing = self.nb - self.next
+        unready = [i for i in range(self.n) if not self.marked[i]]
+        order = list(self.order)
+        self._reset()
+        return missing, unready, order
+
+    def __del__(self):
+        if getattr(self, "L", None) is not None and getattr(self, "h", None):
+            self.L.imr_tracker_free(self.h)
+            self.h = None
+
+
+class DataParallel(nn.Module):
+    def __init__(self, module: nn.Module, arena: ParamArena, comm: Optional[Communicator] = None,
+                 bucket_cap_mb: float = 16.0, first_bucket_mb: float = 2.0,
+                 broadcast_buffers: str = "eval", rebuild_buckets: bool = True,
+                 find_unused_parameters: bool = False, use_autograd_hooks: Optional[bool] = None):
+        super().__init__()
+        self.module = module
+        self.arena = arena
+        self.comm = comm or LocalCommunicator()
+        self.cap = int(bucket_cap_mb * MB)
+        self.first_cap = int(first_bucket_mb * MB)
+        self.broadcast_buffers = broadcast_buffers
+        self.rebuild_pending = rebuild_buckets
+        self.find_unused = find_unused_parameters
+        self.sync_enabled = True
+        self.iteration = 0
+        self._callback_queued = False
+        self._in_backward = False
+        self.last_order: List[int] = []
+
+        self._verify_and_broadcast()
+        self._plan()
+        for i, p in enumerate(self.arena.params):
+            p._imagent_ready = self._mark_param
+            p._imagent_index = i
+        if use_autograd_hooks is None:
+            use_autograd_hooks = getattr(module, "backend", "torch") != "hip"
+        self.hooks = []
+        if use_autograd_hooks:
+            for p in self.arena.params:
+                self.hooks.append(p.register_post_accumulate_grad_hook(self._mark_param))
+
+    # ----------------------------------------------------------- set-up
+    def _verify_and_broadcast(self):
+        ws = self.comm.world_size
+        if ws <= 1:
+            return
+        # shape verification (X2): every rank must hold the same parameter list
+        sig = torch.tensor([hash(tuple((n, s) for n, s in zip(self.arena.names, self.arena.shapes)))
+                            & 0x7FFFFFFFFFFF], dtype=torch.int64, device=self.arena.P.device)
+        allsig = self.comm.allgather(sig)
+        if not bool((allsig == allsig[0]).all()):
+            raise RuntimeError("DataParallel: parameter shapes differ across ranks")
+        # parameters + buffers from rank 0 (X3), one flat broadcast each
+        self.comm.broadcast_(self.arena.P, 0)
+        self.sync_buffers()
+
+    def _plan(self):
+        order = self.arena.order
+        nbytes = [self.arena.nbytes_of(i) for i in order]
+        bid_in_order = plan_buckets(nbytes, self.first_cap, self.cap)
+        nb = (max(bid_in_order) + 1) if bid_in_order else 0
+        bucket_of = [0] * len(order)
+        for pos, i in enumerate(order):
+            bucket_of[i] = bid_in_order[pos]
+        self.bucket_of = bucket_of
+        # contiguous slices of G per bucket
+        self.buckets = []
+        for b in range(nb):
+            members = [i for i in order if bucket_of[i] == b]
+            lo = self.arena.offsets[members[0]]
+            last = members[-1]
+            hi = self.arena.offsets[last] + self.arena.numels[last]
+            self.buckets.append((lo, hi, members))
+        self.tracker = _Tracker(bucket_of, nb)
+
+    def bucket_sizes_mb(self) -> List[float]:
+        return [(hi - lo) * 4 / MB for lo, hi, _ in self.buckets]
+
+    def sync_buffers(self):
+        """Broadcast every buffer (BN running stats, counters) from rank 0."""
+        if self.comm.world_size <= 1:
+            return
+        bufs = [b for b in self.module.buffers()]
+        if not bufs:
+            return
+        dev = self.arena.P.device
+        f = [b for b in bufs if b.dtype == torch.float32]
+        o = [b for b in bufs if b.dtype != torch.float32]
+        if f:
+            flat = torch.cat([b.reshape(-1) for b in f]).to(dev)
+            self.comm.broadcast_(flat, 0)
+            off = 0
+            for b in f:
+                b.copy_(flat[off:off + b.numel()].view_as(b))
+                off += b.numel()
+        if o:
+            flat = torch.cat([b.reshape(-1).to(torch.int64) for b in o]).to(dev)
+            self.comm.broadcast_(flat, 0)
+            off = 0
+            for b in o:
+                b.copy_(flat[off:off + b.numel()].view_as(b))
+                off += b.numel()
+
+    # ---------------------------------------------------------- forward
+    def forward(self, *args, **kw):
+        if self.broadcast_buffers == "always" and self.module.training:
+            self.sync_buffers()
+        return self.module(*args, **kw)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: skip communication inside the context."""
+        prev = self.sync_enabled
+        self.sync_enabled = False
+        try:
+            yield
+        finally:
+            self.sync_enabled = prev
+
+    # --------------------------------------------------------- backward
+    def _mark_param(self, p):
+        if not self.sync_enabled:
+            return
+        i = p._imagent_index
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+        first, count = self.tracker.mark(i)
+        for b in range(first, first + count):
+            self._launch(b)
+
+    def _launch(self, b: int):
+        lo, hi, _ = self.buckets[b]
+        self.comm.allreduce_(self.arena.G[lo:hi], "avg")
+
+    def _finalize_backward(self):
+        self._callback_queued = False
+        missing, unready, order = self.tracker.finalize()
+        if missing:
+            if not self.find_unused:
+                names = [self.arena.names[i] for i in unready][:8]
+                raise RuntimeError(
+                    "DataParallel: expected to have finished reduction in the prior iteration; "
+                    f"{len(unready)} parameters never produced a gradient (e.g. {names}). "
+                    "Pass find_unused_parameters=True if this is intended.")
+            # unused parameters contribute zeros: launch the remaining buckets in order
+            for b in range(len(self.buckets) - missing, len(self.buckets)):
+                self._launch(b)
+        self.comm.join()
+        self.iteration += 1
+        self.last_order = order
+        if self.rebuild_pending and self.iteration == 1 and order:
+            self.rebuild_pending = False
+            self._maybe_rebuild(order)
+
+    def _maybe_rebuild(self, ready_order: List[int]):
+        """Rebuild the layout once from the observed ready order (torch DDP
+        rebuilds its buckets after the first iteration). The optimizer
+        must not own arena-shaped state yet (it is created lazily)."""
+        if ready_order == list(self.arena.order):
+            return
+        seen = set(ready_order)
+        order = list(ready_order) + [i for i in self.arena.order if i not in seen]
+        self.pending_relayout = order
+
+    def apply_pending_relayout(self, flats=()):
+        order = getattr(self, "pending_relayout", None)
+        if order is None:
+            return list(flats)
+        self.pending_relayout = None
+        out = self.arena.relayout(order, flats)
+        self._plan()
+        return out

@@ -1,0 +1,228 @@
+"""Numerics of every HIP kernel vs a plain-PyTorch fp32 reference of the same op.
+
+Inputs are bf16-rounded first, the reference runs in fp32 on those values,
+and the comparison is a relative L2 error sized for bf16 outputs.
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+CONV_SHAPES = [
+    # N, Ci, H, Co, k, s, p
+    (4, 64, 14, 64, 1, 1, 0),
+    (4, 64, 14, 128, 3, 1, 1),
+    (4, 128, 14, 64, 3, 2, 1),
+    (2, 256, 9, 512, 1, 2, 0),
+    (2, 8, 32, 64, 7, 2, 3),      # stem (padded channels)
+    (3, 72, 11, 200, 3, 1, 1),    # ragged M / N / K tails
+    (2, 2048, 1, 1000, 1, 1, 0),  # fc as 1x1 conv
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_dgrad_wgrad(shape):
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd, igemm_wgrad
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(0)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = bf(torch.randn(Co, Ci, k, k, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+
+    stats = torch.zeros(2, Co, device=DEV)
+    y = igemm_fwd(nhwc(x), nhwc(w), s, p, k, k, stats=stats)
+    assert rel(nchw(y), yr) < 1e-2
+    # epilogue BN statistics of the bf16 output
+    yb = nchw(y).float()
+    assert rel(stats[0], yb.sum((0, 2, 3))) < 1e-3
+    assert rel(stats[1], (yb * yb).sum((0, 2, 3))) < 1e-3
+
+    wt = w.permute(1, 2, 3, 0).contiguous()  # [Ci][KH][KW][Co]
+    dx = igemm_dgrad(nhwc(g), wt, (H, H), s, p, k, k)
+    assert rel(nchw(dx), xr.grad) < 1e-2
+
+    dw = torch.zeros(Co, k, k, Ci, device=DEV)
+    igemm_wgrad(nhwc(g), nhwc(x), dw, s, p, k, k)
+    assert rel(dw.permute(0, 3, 1, 2), wr.grad) < 5e-3
+    # accumulation semantics (+=)
+    igemm_wgrad(nhwc(g), nhwc(x), dw, s, p, k, k)
+    assert rel(dw.permute(0, 3, 1, 2), 2 * wr.grad) < 5e-3
+
+
+def test_conv_fwd_bias_fp32_out():
+    from imagent_amd.ops.conv import igemm_fwd
+    torch.manual_seed(1)
+    x = bf(torch.randn(16, 512, device=DEV))
+    w = bf(torch.randn(1000, 512, device=DEV) * 0.05)
+    b = torch.randn(1000, device=DEV)
+    y = igemm_fwd(x.view(16, 1, 1, 512), w.view(1000, 1, 1, 512), 1, 0, 1, 1, bias=b, out_f32=True)
+    ref = x.float() @ w.float().t() + b
+    assert y.dtype == torch.float32
+    assert rel(y.view(16, 1000), ref) < 1e-4
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_bn_fwd_bwd(mode, C):
+    from imagent_amd.models.resnet import BatchNorm2d, BNWork
+    from imagent_amd.ops.bn import BNActFn
+    torch.manual_seed(2)
+    N, H = 4, 7
+    x = bf(torch.randn(N, H, H, C, device=DEV) * 2 + 0.5)
+    x2 = bf(torch.randn(N, H, H, C, device=DEV))
+    bn = BatchNorm2d(C).to(DEV)
+    bn2 = BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn2.weight.uniform_(0.5, 1.5)
+        bn2.bias.uniform_(-0.5, 0.5)
+    for m in (bn, bn2):
+        m.weight.grad = torch.zeros_like(m.weight)
+        m.bias.grad = torch.zeros_like(m.bias)
+    for m, t in ((bn, x), (bn2, x2)):
+        st = torch.stack([t.float().sum((0, 1, 2)), (t.float() ** 2).sum((0, 1, 2))])
+        m.work = BNWork(st, None, torch.zeros(2, C, device=DEV), None, torch.zeros(3, C, device=DEV))
+    xa = x.clone().requires_grad_(True)
+    x2a = x2.clone().requires_grad_(True)
+    y = BNActFn.apply(xa, x2a if mode else None, bn, bn2 if mode == 2 else None, mode, True)
+    g = bf(torch.randn_like(y.float()))
+    y.backward(g)
+
+    # reference
+    xr = nchw(x).float().requires_grad_(True)
+    x2r = nchw(x2).float().requires_grad_(True)
+    gr_w = bn.weight.detach().clone().requires_grad_(True)
+    gr_b = bn.bias.detach().clone().requires_grad_(True)
+    gr_w2 = bn2.weight.detach().clone().requires_grad_(True)
+    gr_b2 = bn2.bias.detach().clone().requires_grad_(True)
+    yr = F.batch_norm(xr, None, None, gr_w, gr_b, True, 0.1, 1e-5)
+    if mode == 1:
+        yr = yr + x2r
+    elif mode == 2:
+        yr = yr + F.batch_norm(x2r, None, None, gr_w2, gr_b2, True, 0.1, 1e-5)
+    yr = F.relu(yr)
+    yr.backward(nchw(g).float())
+    assert rel(nchw(y), yr) < 1e-2
+    assert rel(nchw(xa.grad), xr.grad) < 2e-2
+    assert rel(bn.weight.grad, gr_w.grad) < 1e-2
+    assert rel(bn.bias.grad, gr_b.grad) < 1e-2
+    if mode == 1:
+        assert rel(nchw(x2a.grad), x2r.grad) < 1e-2
+    if mode == 2:
+        assert rel(nchw(x2a.grad), x2r.grad) < 2e-2
+        assert rel(bn2.weight.grad, gr_w2.grad) < 1e-2
+        assert rel(bn2.bias.grad, gr_b2.grad) < 1e-2
+
+
+def test_maxpool_avgpool():
+    from imagent_amd.ops.misc import AvgPoolFn, MaxPoolFn
+    torch.manual_seed(3)
+    x = bf(torch.randn(2, 64, 17, 17, device=DEV))
+    xa = nhwc(x).requires_grad_(True)
+    y = MaxPoolFn.apply(xa, 3, 2, 1)
+    g = bf(torch.randn_like(y.float()))
+    y.backward(g)
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    yr.backward(nchw(g).float())
+    assert rel(nchw(y), yr) == 0.0
+    assert rel(nchw(xa.grad), xr.grad) < 1e-2
+
+    x = bf(torch.randn(3, 7, 7, 256, device=DEV)).requires_grad_(True)
+    p = AvgPoolFn.apply(x)
+    assert rel(p, x.float().mean((1, 2))) < 1e-2
+    gp = bf(torch.randn(3, 256, device=DEV))
+    p.backward(gp)
+    assert rel(x.grad, gp.float()[:, None, None, :].expand(3, 7, 7, 256) / 49) < 1e-2
+
+
+def test_xent_topk():
+    from imagent_amd.ops.misc import XentFn
+    torch.manual_seed(4)
+    z = torch.randn(64, 1000, device=DEV) * 3
+    lab = torch.randint(0, 1000, (64,), device=DEV)
+    lab[:8] = z[:8].argmax(1)  # force some top-1 hits
+    met = torch.zeros(4, device=DEV)
+    za = z.clone().requires_grad_(True)
+    loss = XentFn.apply(za, lab, met, 0.0)
+    loss.backward()
+    zr = z.clone().requires_grad_(True)
+    lr = F.cross_entropy(zr, lab)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 1e-4
+    assert rel(za.grad, zr.grad) < 1e-2
+    top5 = z.topk(5, 1).indices
+    assert met[1].item() == (top5[:, 0] == lab).sum().item()
+    assert met[2].item() == (top5 == lab[:, None]).any(1).sum().item()
+    assert met[3].item() == 64
+    assert abs(met[0].item() - lr.item() * 64) < 1e-2
+
+
+def test_sgd_flat_matches_torch():
+    from imagent_amd.ops.misc import sgd_flat
+    torch.manual_seed(5)
+    n = 10007
+    p = torch.randn(n, device=DEV)
+    ps = [p.clone().requires_grad_(True)]
+    opt = torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    buf = torch.zeros(n, device=DEV)
+    sh = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    for step in range(3):
+        g = torch.randn(n, device=DEV)
+        ps[0].grad = g.clone()
+        opt.step()
+        sgd_flat(p, g, buf, sh, 0.1, 0.9, 0.0, 1e-4, False, step == 0)
+    assert rel(p, ps[0].detach()) < 1e-6
+    assert rel(sh, p) < 1e-2
+
+
+def test_normalize_and_transpose():
+    from imagent_amd.ops.misc import TransposePlan, normalize_u8
+    torch.manual_seed(6)
+    img = torch.randint(0, 256, (3, 40, 50, 3), dtype=torch.uint8, device=DEV)
+    crop = torch.tensor([[1, 2], [0, 0], [5, 7]], dtype=torch.int32, device=DEV)
+    flip = torch.tensor([0, 1, 1], dtype=torch.uint8, device=DEV)
+    out = normalize_u8(img, (32, 40), 8, (0.5, 0.5, 0.5), (0.5, 0.5, 0.5), crop, flip)
+    ref = torch.zeros(3, 32, 40, 8, device=DEV)
+    for b in range(3):
+        oy, ox = crop[b].tolist()
+        t = img[b, oy:oy + 32, ox:ox + 40].float() / 255
+        if flip[b]:
+            t = t.flip(1)
+        ref[b, ..., :3] = (t - 0.5) / 0.5
+    assert rel(out, ref) < 5e-3
+    a = bf(torch.randn(96, 9, 40, device=DEV))
+    b = torch.empty(40, 9, 96, device=DEV, dtype=torch.bfloat16)
+    c = bf(torch.randn(1000, 1, 64, device=DEV))
+    d = torch.empty(64, 1, 1000, device=DEV, dtype=torch.bfloat16)
+    TransposePlan([(a, b, 96, 9, 40), (c, d, 1000, 1, 64)], DEV).run()
+    assert torch.equal(b, a.permute(2, 1, 0))
+    assert torch.equal(d, c.permute(2, 1, 0))
