@@ -80,6 +80,11 @@ class NativeState:
         s = self.model.conv1
         s.w_pad[..., : s.in_channels].copy_(s.w_bf16_real)
 
+    def rebind(self) -> None:
+        """After an arena re-layout (bucket rebuild): re-point every shadow."""
+        self._bind_shadows()
+        self.refresh_shadows(full=True)
+
     # ---------------------------------------------------------- workspace
     def _bind_workspace(self):
         bns: List[BatchNorm2d] = self.model.batchnorms()

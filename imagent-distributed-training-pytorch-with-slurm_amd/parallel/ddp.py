@@ -31,6 +31,7 @@ MI355X design:
 from __future__ import annotations
 
 import contextlib
+import zlib
 import ctypes as C
 from typing import Dict, List, Optional
 
@@ -165,8 +166,9 @@ class DataParallel(nn.Module):
         if ws <= 1:
             return
         # shape verification (X2): every rank must hold the same parameter list
-        sig = torch.tensor([hash(tuple((n, s) for n, s in zip(self.arena.names, self.arena.shapes)))
-                            & 0x7FFFFFFFFFFF], dtype=torch.int64, device=self.arena.P.device)
+        desc = repr([(n, s) for n, s in zip(self.arena.names, self.arena.shapes)]).encode()
+        sig = torch.tensor([zlib.crc32(desc), len(self.arena.names)], dtype=torch.int64,
+                           device=self.arena.P.device)
         allsig = self.comm.allgather(sig)
         if not bool((allsig == allsig[0]).all()):
             raise RuntimeError("DataParallel: parameter shapes differ across ranks")
@@ -277,10 +279,15 @@ class DataParallel(nn.Module):
         """Rebuild the layout once from the observed ready order (torch DDP
         rebuilds its buckets after the first iteration). The optimizer
         must not own arena-shaped state yet (it is created lazily)."""
-        if ready_order == list(self.arena.order):
-            return
         seen = set(ready_order)
         order = list(ready_order) + [i for i in self.arena.order if i not in seen]
+        if self.comm.world_size > 1:
+            # every rank must use the SAME layout: take rank 0's observed order
+            t = torch.tensor(order, dtype=torch.int64, device=self.arena.P.device)
+            self.comm.broadcast_(t, 0)
+            order = t.tolist()
+        if order == list(self.arena.order):
+            return
         self.pending_relayout = order
 
     def apply_pending_relayout(self, flats=()):

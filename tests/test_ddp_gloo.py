@@ -1,0 +1,85 @@
+"""Multi-process (gloo, CPU) data parallelism: our bucketed DataParallel over the
+flat arena vs torch.nn.parallel.DistributedDataParallel (imagenet.py:316)."""
+
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir, bucket_mb, rebuild):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from imagent_amd.models import resnet
+    from imagent_amd.models.arena import ParamArena
+    from imagent_amd.parallel.comm import TorchCommunicator
+    from imagent_amd.parallel.ddp import DataParallel
+    from imagent_amd.train.optim import FlatSGD
+
+    torch.manual_seed(1234 + rank)           # DIFFERENT init per rank: the broadcast must fix it
+    ours = resnet.resnet18(num_classes=10)
+    torch.manual_seed(99)
+    ref = resnet.resnet18(num_classes=10)
+    order = list(reversed(range(len(list(ours.parameters())))))
+    arena = ParamArena(list(ours.named_parameters()), "cpu", order=order)
+    ddp = DataParallel(ours, arena, TorchCommunicator(), bucket_cap_mb=bucket_mb, first_bucket_mb=0.5,
+                       rebuild_buckets=rebuild)
+    # reference model starts from OUR rank-0 weights
+    with torch.no_grad():
+        for a, b in zip(ref.parameters(), ours.parameters()):
+            a.copy_(b)
+        for a, b in zip(ref.buffers(), ours.buffers()):
+            a.copy_(b)
+    ref_ddp = torch.nn.parallel.DistributedDataParallel(ref, broadcast_buffers=False)
+    opt = FlatSGD(arena, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(rank)
+    maxdiff = 0.0
+    for step in range(3):
+        x = torch.randn(4, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        opt.zero_grad()
+        F.cross_entropy(ddp(x), y).backward()
+        if getattr(ddp, "pending_relayout", None) is not None:
+            opt.set_flats(ddp.apply_pending_relayout(opt.flats()))
+        ropt.zero_grad()
+        F.cross_entropy(ref_ddp(x), y).backward()
+        for (n, a), b in zip(ours.named_parameters(), ref.parameters()):
+            d = (a.grad - b.grad).abs().max().item() / (b.grad.abs().max().item() + 1e-12)
+            maxdiff = max(maxdiff, d)
+        opt.step()
+        ropt.step()
+    pdiff = max((a - b).abs().max().item() for a, b in zip(ours.parameters(), ref.parameters()))
+    with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
+        f.write(f"{maxdiff} {pdiff} {len(ddp.buckets)} {ddp.iteration}\n")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb,rebuild", [(1.0, False), (4.0, True)])
+def test_grads_match_torch_ddp(bucket_mb, rebuild):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d, bucket_mb, rebuild), nprocs=world,
+                           start_method="spawn", join=True)
+        for r in range(world):
+            gd, pd, nb, it = open(os.path.join(d, f"r{r}.txt")).read().split()
+            assert float(gd) < 1e-4, gd
+            assert float(pd) < 1e-5, pd
+            assert int(nb) > 1 and int(it) == 3

@@ -1,4 +1,10 @@
-"""Whole-network parity: HIP NHWC bf16 path vs the PyTorch fp32 NCHW oracle."""
+"""Whole-network parity: HIP NHWC bf16 path vs the PyTorch fp32 NCHW oracle.
+
+bf16 end-to-end training gradients differ from fp32 ones by an amount that
+grows towards the stem (errors accumulate through the backward). The yardstick
+is therefore PyTorch's OWN bf16 path (autocast, MIOpen): per parameter, the
+HIP path's error vs fp32 must be comparable to autocast-bf16's error vs fp32.
+"""
 
 import copy
 
@@ -14,6 +20,15 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
+def _grads(model, x, lab, autocast=False):
+    for p in model.parameters():
+        p.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        logits = model(x)
+    F.cross_entropy(logits.float(), lab).backward()
+    return logits.float(), {n: p.grad.float().clone() for n, p in model.named_parameters()}
+
+
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_hip_vs_torch_forward_backward(arch):
     from imagent_amd.models import resnet
@@ -23,14 +38,11 @@ def test_hip_vs_torch_forward_backward(arch):
     ref = resnet.build(arch, num_classes=1000).to(DEV)
     model = copy.deepcopy(ref)
     st = bind_native(model, DEV)
-    # make the reference see exactly the bf16-rounded weights the kernels use
-    with torch.no_grad():
+    with torch.no_grad():  # the oracle sees exactly the bf16-rounded weights the kernels use
         for p_ref, p in zip(ref.parameters(), model.parameters()):
             p_ref.copy_(p.to(torch.bfloat16).float())
-    B, H = 8, 64
-    # spatially smooth images: with white noise, bf16-vs-fp32 argmax flips in
-    # the stem maxpool route gradient to UNCORRELATED neighbour pixels, which
-    # dominates the stem weight-gradient error and hides real bugs
+    ref_bf = copy.deepcopy(ref)
+    B, H = 16, 64
     low = torch.rand(B, 3, 8, 8, device=DEV)
     img = (F.interpolate(low, size=(H, H), mode="bicubic", align_corners=False).clamp(0, 1) * 255)
     img = img.to(torch.uint8).permute(0, 2, 3, 1).contiguous()
@@ -40,31 +52,35 @@ def test_hip_vs_torch_forward_backward(arch):
 
     model.train()
     ref.train()
+    ref_bf.train()
     st.arena.zero_grad()
     logits = model(x)
-    loss = F.cross_entropy(logits, lab)
-    loss.backward()
-    for p in ref.parameters():
-        p.grad = None
-    lr_ = ref(xr)
-    lref = F.cross_entropy(lr_, lab)
-    lref.backward()
-    assert rel(logits, lr_) < 5e-2, rel(logits, lr_)
-    # gradients of a representative set of parameters
-    named_ref = dict(ref.named_parameters())
-    worst = 0.0
+    F.cross_entropy(logits, lab).backward()
+    l32, g32 = _grads(ref, xr, lab)
+    lbf, gbf = _grads(ref_bf, xr, lab, autocast=True)
+    e_log, e_log_bf = rel(logits, l32), rel(lbf, l32)
+    print(f"logits: hip {e_log:.4f} autocast-bf16 {e_log_bf:.4f}")
+    assert e_log < max(5e-2, 2.0 * e_log_bf), (e_log, e_log_bf)
+    bad = []
+    report = []
     for name, p in model.named_parameters():
-        e = rel(p.grad, named_ref[name].grad)
-        worst = max(worst, e)
-        assert e < 0.15, (name, e)
-    # running statistics were updated like nn.BatchNorm2d
-    for (n1, b1), (n2, b2) in zip(model.named_buffers(), ref.named_buffers()):
+        e_hip = rel(p.grad, g32[name])
+        e_bf = rel(gbf[name], g32[name])
+        report.append((name, round(e_hip, 4), round(e_bf, 4)))
+        if e_hip > max(0.05, 2.0 * e_bf):
+            bad.append(report[-1])
+    print("\n".join(str(r) for r in report))
+    assert not bad, bad
+    for (n1, b1), (n2, b2), (_, b3) in zip(model.named_buffers(), ref.named_buffers(),
+                                           ref_bf.named_buffers()):
         if "num_batches_tracked" in n1:
-            assert b1.item() == b2.item() == 1
+            assert b1.item() == 1
         else:
-            assert rel(b1, b2) < 2e-2, n1
-    # eval path
+            assert rel(b1, b2) < max(2e-2, 2.0 * rel(b3, b2)), n1
     model.eval()
     ref.eval()
+    ref_bf.eval()
     with torch.no_grad():
-        assert rel(model(x), ref(xr)) < 5e-2
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ebf = rel(ref_bf(xr).float(), ref(xr))
+        assert rel(model(x), ref(xr)) < max(5e-2, 2.0 * ebf)
