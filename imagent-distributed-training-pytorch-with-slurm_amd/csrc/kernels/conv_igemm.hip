@@ -50,13 +50,14 @@ struct IGemmArgs {
 
 #define IG_OUT_F32 1
 #define IG_RELU 2
+#define IG_STEM 4
 
 namespace {
 
 constexpr int BK = 64;
 constexpr int LDK = BK + 8;  // padded row (elements): 144 B
 
-template <int BM, int BN, int WN, bool ALIGNED>
+template <int BM, int BN, int WN, int MODE>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     constexpr int WM = 4 / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bn = bid % nbn, bm = bid / nbn;
     const int m0 = bm * BM, n0 = bn * BN;
-    const int K = a.nth * a.ntw * a.C;
+    const int K = MODE == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
     const int nk = (K + BK - 1) / BK;
     const int col8 = tid & 7;
     const int ohw = a.OH * a.OW;
@@ -103,9 +104,35 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
 
     u32x4 rx[A_CH], rw[B_CH];
     auto load_tile = [&](int kt) {
+        if (MODE == 2) {
+            // stem: C == 4 and the KW taps x 4 channels of one kernel row are
+            // contiguous in NHWC memory; K = KH rows x 32 (28 real + 4 zero).
+            const int kh = kt * 2 + (col8 >> 2);
+            const int seg = (col8 & 3) * 8, kw0 = seg >> 2;
+            const bool kok = kh < a.nth;
+#pragma unroll
+            for (int i = 0; i < A_CH; ++i) {
+                const int ih = ih0[i] + a.dh0 + kh, iw = iw0[i] + a.dw0 + kw0;
+                const bool rok = kok && mok[i] && (unsigned)ih < (unsigned)a.H;
+                const bool lo_ok = rok && kw0 < a.ntw && (unsigned)iw < (unsigned)a.W;
+                const bool hi_ok = rok && kw0 + 1 < a.ntw && (unsigned)(iw + 1) < (unsigned)a.W;
+                const long off = ((long)ih * a.W + iw) * 4;
+                u32x2 lo = {0, 0}, hi = {0, 0};
+                if (lo_ok) lo = *reinterpret_cast<const u32x2*>(xrow[i] + off);
+                if (hi_ok) hi = *reinterpret_cast<const u32x2*>(xrow[i] + off + 4);
+                rx[i] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+            }
+#pragma unroll
+            for (int j = 0; j < B_CH; ++j) {
+                u32x4 v = {0, 0, 0, 0};
+                if (kok && nok[j]) v = *reinterpret_cast<const u32x4*>(wrow[j] + kh * 32 + seg);
+                rw[j] = v;
+            }
+            return;
+        }
         const int k = kt * BK + col8 * 8;
         int t, c;
-        if (ALIGNED) {  // C % 64 == 0: the whole K tile sits in one tap
+        if (MODE == 0) {  // C % 64 == 0: the whole K tile sits in one tap
             t = (kt * BK) / a.C;
             c = kt * BK - t * a.C + col8 * 8;
         } else {
@@ -257,11 +284,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     }
 }
 
-template <int BM, int BN, int WN, bool AL>
+template <int BM, int BN, int WN, int MD>
 int launch(const IGemmArgs& a, hipStream_t st) {
     const int nbm = (a.M + BM - 1) / BM, nbn = (a.Nout + BN - 1) / BN;
     const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
-    hipLaunchKernelGGL((igemm_kernel<BM, BN, WN, AL>), dim3(nbm * nbn), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, WN, MD>), dim3(nbm * nbn), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -272,16 +299,22 @@ int launch(const IGemmArgs& a, hipStream_t st) {
 IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const IGemmArgs& a = *args;
     hipStream_t st = (hipStream_t)stream;
-    if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     if (a.M <= 0 || a.Nout <= 0) return 0;
-    const bool al = (a.C % BK) == 0;
+    if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32
+        if (a.C != 4 || a.ntw > 8 || a.dhs != 1 || a.dws != 1) return -102;
+        return launch<256, 64, 1, 2>(a, st);
+    }
+    if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
+    const int md = (a.C % BK) == 0 ? 0 : 1;
     if (tile == 0) tile = (a.Nout <= 64) ? 1 : 2;
+#define IG_L(BM_, BN_, WN_) (md == 0 ? launch<BM_, BN_, WN_, 0>(a, st) : launch<BM_, BN_, WN_, 1>(a, st))
     switch (tile) {
-        case 1: return al ? launch<256, 64, 1, true>(a, st) : launch<256, 64, 1, false>(a, st);
-        case 2: return al ? launch<128, 128, 2, true>(a, st) : launch<128, 128, 2, false>(a, st);
-        case 3: return al ? launch<64, 128, 4, true>(a, st) : launch<64, 128, 4, false>(a, st);
+        case 1: return IG_L(256, 64, 1);
+        case 2: return IG_L(128, 128, 2);
+        case 3: return IG_L(64, 128, 4);
         default: return -101;
     }
+#undef IG_L
 }
 
 IMK_EXPORT int imk_igemm_args_size() { return (int)sizeof(IGemmArgs); }

@@ -33,6 +33,7 @@ struct WgradArgs {
     int KH, KW, stride, pad;
     int m_per_split;   // multiple of BR
     uint32_t mg_ohw, sh_ohw, mg_ow, sh_ow;  // magic division by OH*OW and OW
+    int stem;          // 1: C == 4 row-segment gather, dW is [Co][KH][32]
 };
 
 namespace {
@@ -43,7 +44,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
     return (uint32_t)(((uint64_t)__umulhi(n, mg) + n) >> sh);
 }
 
-template <int BCO, int BKC, int WCO>
+template <int BCO, int BKC, int WCO, bool STEM>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
     constexpr int WKC = 4 / WCO;
     constexpr int TCO = BCO / WCO, TKC = BKC / WKC;
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wco = wid % WCO, wkc = wid / WCO;
-    const int K = a.KH * a.KW * a.Ci;
+    const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int nco = (a.Co + BCO - 1) / BCO, nkc = (K + BKC - 1) / BKC;
     const int ntiles = nco * nkc;
     const int bid = blockIdx.x;
@@ -77,10 +78,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
     const int xcol = tid % CPR_X;
     const int xk = kc0 + xcol * 8;
     const bool xk_ok = xk < K;
-    const int xtap = xk_ok ? xk / a.Ci : 0;
-    const int xci = xk - xtap * a.Ci;
-    const int xkh = xtap / a.KW, xkw = xtap - xkh * a.KW;
-    const int xdh = xkh - a.pad, xdw = xkw - a.pad;
+    int xci, xdh, xdw, xkw0 = 0;
+    if (STEM) {  // column = kh*32 + kw*4 + c
+        const int kh = xk / 32, seg = xk - kh * 32;
+        xkw0 = seg >> 2;
+        xci = 0;
+        xdh = kh - a.pad;
+        xdw = xkw0 - a.pad;
+    } else {
+        const int xtap = xk_ok ? xk / a.Ci : 0;
+        xci = xk - xtap * a.Ci;
+        const int xkh = xtap / a.KW, xkw = xtap - xkh * a.KW;
+        xdh = xkh - a.pad;
+        xdw = xkw - a.pad;
+    }
 
     u32x4 rd[D_CH], rx[X_CH];
     auto load = [&](int st) {
@@ -104,8 +115,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
                 const uint32_t oh = fdiv(rem, a.mg_ow, a.sh_ow);
                 const uint32_t ow = rem - oh * (uint32_t)a.OW;
                 const int ih = (int)oh * a.stride + xdh, iw = (int)ow * a.stride + xdw;
-                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                if (STEM) {
+                    if ((unsigned)ih < (unsigned)a.H) {
+                        const bf16_t* p = a.X + (((long)img * a.H + ih) * a.W + iw) * 4;
+                        u32x2 lo = {0, 0}, hi = {0, 0};
+                        if (xkw0 < a.KW && (unsigned)iw < (unsigned)a.W) lo = *reinterpret_cast<const u32x2*>(p);
+                        if (xkw0 + 1 < a.KW && (unsigned)(iw + 1) < (unsigned)a.W)
+                            hi = *reinterpret_cast<const u32x2*>(p + 4);
+                        v = u32x4{lo[0], lo[1], hi[0], hi[1]};
+                    }
+                } else if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
                     v = *reinterpret_cast<const u32x4*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.Ci + xci);
+                }
             }
             rx[i] = v;
         }
@@ -195,9 +216,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         }
 }
 
-template <int BCO, int BKC, int WCO>
+template <int BCO, int BKC, int WCO, bool STEM>
 int launch(WgradArgs a, int splits, hipStream_t st) {
-    const int K = a.KH * a.KW * a.Ci;
+    const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
     if (splits <= 0) {
         // ~3 blocks per CU over 256 CUs, at least 4 stages per block
@@ -210,7 +231,7 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
-    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO>), dim3(ntiles * splits), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM>), dim3(ntiles * splits), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -219,11 +240,15 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
 
 IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     const WgradArgs& a = *args;
-    if (a.Ci % 8 || a.Co % 8) return -100;
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (a.Co <= 64) return launch<64, 128, 1>(a, splits, st);
-    return launch<128, 128, 2>(a, splits, st);
+    if (a.stem) {
+        if (a.Ci != 4 || a.KW > 8 || a.Co % 8) return -102;
+        return launch<64, 128, 1, true>(a, splits, st);
+    }
+    if (a.Ci % 8 || a.Co % 8) return -100;
+    if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
+    return launch<128, 128, 2, false>(a, splits, st);
 }
 
 IMK_EXPORT int imk_wgrad_args_size() { return (int)sizeof(WgradArgs); }

@@ -64,7 +64,7 @@ def decode_resize(path: str, size: Tuple[int, int]) -> np.ndarray:
         img = img.convert("RGB")
         if img.size != (size[1], size[0]):
             img = img.resize((size[1], size[0]), Image.BILINEAR)
-        return np.asarray(img, dtype=np.uint8)
+        return np.array(img, dtype=np.uint8)  # writable copy
 
 
 class ImageFolderU8(torch.utils.data.Dataset):

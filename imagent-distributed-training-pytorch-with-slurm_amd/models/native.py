@@ -23,6 +23,12 @@ from .arena import ParamArena
 from .resnet import BasicBlock, BatchNorm2d, BNWork, Bottleneck, Conv2d, Linear, ResNet
 
 
+def stem_view(t: torch.Tensor, kw: int) -> torch.Tensor:
+    """[Co][KH][32] stem weight/grad -> [Co][KH][KW][4] view of its real taps."""
+    co, kh, _ = t.shape
+    return t[:, :, : kw * 4].view(co, kh, kw, 4)  # splits the unit-stride dim: stays a view
+
+
 class NativeState:
     def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None):
         self.device = torch.device(device)
@@ -61,11 +67,11 @@ class NativeState:
         fc.wt_bf16 = self.T[off:off + n].view(fc.in_features, fc.out_features)
         st_items.append((fc.w_bf16, fc.wt_bf16, fc.out_features, 1, fc.in_features))
         self.tplan = TransposePlan(st_items, dev)
-        # stem: pad Ci 3 -> 8
+        # stem: input channels 3 -> 4, kernel row = 7 taps x 4 ch padded to 32
         s = m.conv1
-        cp = ResNet.STEM_CPAD
-        s.w_pad = torch.zeros((s.out_channels, s.kh, s.kw, cp), dtype=torch.bfloat16, device=dev)
-        s.grad_pad = torch.zeros((s.out_channels, s.kh, s.kw, cp), dtype=torch.float32, device=dev)
+        s.stem = True
+        s.w_pad = torch.zeros((s.out_channels, s.kh, 32), dtype=torch.bfloat16, device=dev)
+        s.grad_pad = torch.zeros((s.out_channels, s.kh, 32), dtype=torch.float32, device=dev)
         s.w_bf16_real = s.w_bf16
         s.w_bf16 = s.w_pad
 
@@ -78,7 +84,7 @@ class NativeState:
             cast_bf16(self.arena.P, self.arena.S)
         self.tplan.run()
         s = self.model.conv1
-        s.w_pad[..., : s.in_channels].copy_(s.w_bf16_real)
+        stem_view(s.w_pad, s.kw)[..., : s.in_channels].copy_(s.w_bf16_real)
 
     def rebind(self) -> None:
         """After an arena re-layout (bucket rebuild): re-point every shadow."""

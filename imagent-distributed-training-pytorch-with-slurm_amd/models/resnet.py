@@ -161,7 +161,9 @@ class Bottleneck(nn.Module):
 # --------------------------------------------------------------------------
 
 class ResNet(nn.Module):
-    STEM_CPAD = 8  # NHWC input channels on the HIP path (3 real + 5 zero)
+    # NHWC input channels on the HIP path (3 real + 1 zero): the stem kernel
+    # reads the 7 taps x 4 channels of a kernel row as one contiguous segment
+    STEM_CPAD = 4
 
     def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int],
                  num_classes: int = 1000, zero_init_residual: bool = False):

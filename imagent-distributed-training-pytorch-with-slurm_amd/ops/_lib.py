@@ -95,6 +95,7 @@ class WgradArgs(C.Structure):
         ("KH", C.c_int), ("KW", C.c_int), ("stride", C.c_int), ("pad", C.c_int),
         ("m_per_split", C.c_int),
         ("mg_ohw", C.c_uint32), ("sh_ohw", C.c_uint32), ("mg_ow", C.c_uint32), ("sh_ow", C.c_uint32),
+        ("stem", C.c_int),
     ]
 
 

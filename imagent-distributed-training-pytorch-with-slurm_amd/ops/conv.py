@@ -48,21 +48,26 @@ def _base_args(x_ptr, w_ptr, y_ptr, N, H, W, Cin, OH, OW, Nout, ldb, sA) -> _lib
 def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
               stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
-              tile: int = 0) -> torch.Tensor:
+              tile: int = 0, stem: bool = False) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
-    per-channel (sum, sumsq) accumulation into ``stats`` [2, Co]."""
+    per-channel (sum, sumsq) accumulation into ``stats`` [2, Co].
+
+    ``stem``: x has 4 channels and w is ``[Co][KH][32]`` (row = KW taps x 4
+    channels, zero padded) - the row-segment gather of the 7x7 stem."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
     if out is None:
         out = torch.empty((N, OH, OW, Co), device=x.device,
                           dtype=torch.float32 if out_f32 else torch.bfloat16)
-    a = _base_args(x.data_ptr(), w.data_ptr(), out.data_ptr(), N, H, W, Ci, OH, OW, Co, KH * KW * Ci,
-                   stride)
+    if stem:
+        assert Ci == 4 and tuple(w.shape) == (Co, KH, 32), (x.shape, w.shape)
+    a = _base_args(x.data_ptr(), w.data_ptr(), out.data_ptr(), N, H, W, Ci, OH, OW, Co,
+                   KH * 32 if stem else KH * KW * Ci, stride)
     a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = KH, KW, -pad, 1, -pad, 1
     a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
-    a.flags = (1 if out_f32 else 0) | (2 if relu else 0)
+    a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0)
     if bias is not None:
         a.bias = bias.data_ptr()
     if stats is not None:
@@ -110,11 +115,15 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
 
 
 def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int, KH: int,
-                KW: int, splits: int = 0) -> None:
-    """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci])."""
+                KW: int, splits: int = 0, stem: bool = False) -> None:
+    """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci]).
+    ``stem``: x has 4 channels, dw is ``[Co][KH][32]`` (see :func:`igemm_fwd`)."""
     N, H, W, Ci = x.shape
     _, OH, OW, Co = dy.shape
+    if stem:
+        assert Ci == 4 and dw.numel() == Co * KH * 32
     a = _lib.WgradArgs()
+    a.stem = 1 if stem else 0
     a.dY, a.X, a.dW = dy.data_ptr(), x.data_ptr(), dw.data_ptr()
     a.N, a.H, a.W, a.Ci, a.Co = N, H, W, Ci, Co
     a.OH, a.OW, a.M = OH, OW, N * OH * OW
@@ -143,7 +152,8 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, mod, stats):
-        y = igemm_fwd(x, mod.w_bf16, mod.stride, mod.padding, mod.kh, mod.kw, stats=stats)
+        y = igemm_fwd(x, mod.w_bf16, mod.stride, mod.padding, mod.kh, mod.kw, stats=stats,
+                      stem=getattr(mod, "stem", False))
         ctx.mod = mod
         ctx.save_for_backward(x)
         return y
@@ -158,10 +168,11 @@ class ConvFn(torch.autograd.Function):
             dx = igemm_dgrad(dy, mod.wt_bf16, (x.shape[1], x.shape[2]), mod.stride, mod.padding, mod.kh,
                              mod.kw)
         gp = getattr(mod, "grad_pad", None)
-        if gp is not None:  # stem: input channels padded 3 -> 8 for 16-B NHWC loads
+        if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
             gp.zero_()
-            igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw)
-            mod.weight.grad.permute(0, 2, 3, 1).add_(gp[..., : mod.in_channels])
+            igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw, stem=True)
+            real = gp[:, :, : mod.kw * 4].view(gp.shape[0], mod.kh, mod.kw, 4)[..., : mod.in_channels]
+            mod.weight.grad.permute(0, 2, 3, 1).add_(real)
         else:
             igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw)
         notify_ready(mod.weight)

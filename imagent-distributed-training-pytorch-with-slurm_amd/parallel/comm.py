@@ -146,6 +146,8 @@ class RcclCommunicator(Communicator):
 
     def allreduce_(self, t, op="sum"):
         assert t.is_cuda and t.is_contiguous()
+        if self.world_size == 1:
+            return  # a one-rank all-reduce is the identity: skip the RCCL copy kernel
         self._chk(self.L.imc_allreduce(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], self._cur()),
                   "allreduce")
         # keep the tensor alive until the comm stream is done with it

@@ -1,0 +1,114 @@
+"""Per-layer conv microbenchmark: HIP kernels (fwd / dgrad / wgrad) vs MIOpen.
+
+python scripts/conv_bench.py --arch resnet50 --batch 256 [--miopen]
+Prints one line per unique conv shape with time, TFLOP/s and the HBM roofline
+time (operand + result bytes at 6 TB/s) so the optimisation target is clear.
+"""
+
+import argparse
+import collections
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+
+def shapes(arch, B, size):
+    from imagent_amd.models import resnet
+    m = resnet.build(arch)
+    out = collections.OrderedDict()
+    h = size // 2  # after stem conv
+    # walk the forward to get input spatial sizes
+    hw = {}
+    x = size
+
+    def add(conv, H):
+        key = (conv.in_channels, H, conv.out_channels, conv.kh, conv.stride, conv.padding)
+        out[key] = out.get(key, 0) + 1
+
+    add(m.conv1, size)
+    H = (size + 1) // 2 // 2 + (0 if size % 4 else 0)
+    H = ((size + 6 - 7) // 2 + 1 + 2 - 3) // 2 + 1
+    for b in m.blocks():
+        Hin = H
+        for conv, _, _ in b.convs_bns():
+            add(conv, H)
+            H = (H + 2 * conv.padding - conv.kh) // conv.stride + 1
+        if b.downsample is not None:
+            add(b.downsample[0], Hin)
+    return out
+
+
+def timeit(fn, reps=10, warm=3):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--size", type=int, default=224)
+    ap.add_argument("--miopen", action="store_true")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
+    dev = "cuda"
+    tot = collections.defaultdict(float)
+    rows = []
+    print(f"{'Ci':>5} {'H':>4} {'Co':>5} k s | cnt | {'fwd us':>8} {'TF':>6} {'roof':>6} | {'dgrad':>8} {'TF':>6} | "
+          f"{'wgrad':>8} {'TF':>6}" + (" | miopen fwd" if a.miopen else ""))
+    for (Ci, H, Co, k, s, p), cnt in shapes(a.arch, a.batch, a.size).items():
+        stem = Ci == 3
+        Cin = 4 if stem else Ci
+        B = a.batch
+        OH = conv_out_size(H, k, s, p)
+        x = torch.randn(B, H, H, Cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, k, k, Cin, device=dev) * 0.05).to(torch.bfloat16)
+        if stem:
+            w = torch.zeros(Co, k, 32, device=dev, dtype=torch.bfloat16)
+        wt = w.permute(3, 1, 2, 0).contiguous() if not stem else None
+        dy = torch.randn(B, OH, OH, Co, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(Co, k, 32, device=dev) if stem else torch.zeros(Co, k, k, Cin, device=dev)
+        stats = torch.zeros(2, Co, device=dev)
+        flops = 2.0 * B * OH * OH * Co * k * k * Ci
+        t_f = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, stem=stem))
+        t_d = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k)) if not stem else 0.0
+        t_w = timeit(lambda: igemm_wgrad(dy, x, dw, s, p, k, k, stem=stem))
+        roof = (x.numel() * 2 + dy.numel() * 2 + w.numel() * 2) / 6e12 * 1e6
+        line = (f"{Ci:5d} {H:4d} {Co:5d} {k} {s} | {cnt:3d} | {t_f:8.1f} {flops / t_f / 1e6:6.0f} {roof:6.1f} | "
+                f"{t_d:8.1f} {flops / max(t_d, 1e-9) / 1e6:6.0f} | {t_w:8.1f} {flops / t_w / 1e6:6.0f}")
+        r = dict(Ci=Ci, H=H, Co=Co, k=k, s=s, cnt=cnt, fwd_us=t_f, dgrad_us=t_d, wgrad_us=t_w, gflop=flops / 1e9,
+                 roof_us=roof)
+        if a.miopen:
+            xc = x[..., :Ci].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            wc = (torch.randn(Co, Ci, k, k, device=dev) * 0.05).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+            t_m = timeit(lambda: F.conv2d(xc, wc, None, s, p))
+            line += f" | {t_m:8.1f}"
+            r["miopen_fwd_us"] = t_m
+        print(line, flush=True)
+        rows.append(r)
+        tot["fwd"] += t_f * cnt
+        tot["dgrad"] += t_d * cnt
+        tot["wgrad"] += t_w * cnt
+        tot["miopen"] += r.get("miopen_fwd_us", 0) * cnt
+    print("totals (us, per step):", {k: round(v, 1) for k, v in tot.items()})
+    if a.json:
+        json.dump(dict(rows=rows, totals=tot), open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

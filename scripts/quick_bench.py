@@ -54,7 +54,7 @@ def bench_hip(arch, B, steps, warmup, size):
     first = [True]
 
     def step():
-        x = normalize_u8(img, (size, size), 8, (0.5,) * 3, (0.5,) * 3)
+        x = normalize_u8(img, (size, size), 4, (0.5,) * 3, (0.5,) * 3)
         ar.zero_grad()
         loss = XentFn.apply(m(x), y, met, 0.0)
         loss.backward()

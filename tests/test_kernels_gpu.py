@@ -76,6 +76,34 @@ def test_conv_fwd_dgrad_wgrad(shape):
     assert rel(dw.permute(0, 3, 1, 2), 2 * wr.grad) < 5e-3
 
 
+def test_stem_row_segment_conv():
+    """7x7/s2 stem: 4-channel NHWC input, [Co][KH][32] weight rows (fwd + wgrad)."""
+    from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
+    torch.manual_seed(7)
+    N, H, Co = 3, 38, 64
+    x3 = bf(torch.randn(N, 3, H, H, device=DEV))
+    w3 = bf(torch.randn(Co, 3, 7, 7, device=DEV) * 0.1)
+    xr = x3.float().requires_grad_(True)
+    wr = w3.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 2, 3)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    x4 = torch.zeros(N, H, H, 4, device=DEV, dtype=torch.bfloat16)
+    x4[..., :3] = nhwc(x3)
+    wrow = torch.zeros(Co, 7, 32, device=DEV, dtype=torch.bfloat16)
+    wrow[:, :, :28].view(Co, 7, 7, 4)[..., :3] = w3.permute(0, 2, 3, 1)
+    stats = torch.zeros(2, Co, device=DEV)
+    y = igemm_fwd(x4, wrow, 2, 3, 7, 7, stats=stats, stem=True)
+    assert rel(nchw(y), yr) < 1e-2
+    assert rel(stats[0], nchw(y).float().sum((0, 2, 3))) < 1e-3
+    dw = torch.zeros(Co, 7, 32, device=DEV)
+    igemm_wgrad(nhwc(g), x4, dw, 2, 3, 7, 7, stem=True)
+    got = dw[:, :, :28].reshape(Co, 7, 7, 4)[..., :3].permute(0, 3, 1, 2)
+    assert rel(got, wr.grad) < 5e-3
+    assert dw[:, :, 28:].abs().max().item() == 0.0
+    assert dw[:, :, :28].reshape(Co, 7, 7, 4)[..., 3].abs().max().item() == 0.0
+
+
 def test_conv_fwd_bias_fp32_out():
     from imagent_amd.ops.conv import igemm_fwd
     torch.manual_seed(1)

@@ -47,7 +47,7 @@ def test_hip_vs_torch_forward_backward(arch):
     img = (F.interpolate(low, size=(H, H), mode="bicubic", align_corners=False).clamp(0, 1) * 255)
     img = img.to(torch.uint8).permute(0, 2, 3, 1).contiguous()
     lab = torch.randint(0, 1000, (B,), device=DEV)
-    x = normalize_u8(img, (H, H), 8, (0.5,) * 3, (0.5,) * 3)
+    x = normalize_u8(img, (H, H), 4, (0.5,) * 3, (0.5,) * 3)
     xr = x[..., :3].float().permute(0, 3, 1, 2).contiguous()
 
     model.train()
