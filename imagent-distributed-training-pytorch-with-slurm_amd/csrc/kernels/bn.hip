@@ -320,6 +320,26 @@ IMK_EXPORT int imk_bn_running_update(const void* descs, int n, void* stream) {
 
 IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
 
+// Fold the conv epilogue's [S][2][C] statistics slab into [2][C] sums.
+namespace {
+__global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __restrict__ slab,
+                                                             float* __restrict__ out, int S, int n2c) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n2c) return;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += slab[(size_t)k * n2c + i];
+    out[i] = s;
+}
+}  // namespace
+
+IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C, void* stream) {
+    const int n2c = 2 * C;
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2c + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       slab, out, S, n2c);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
 // scratch: fp32 [3][C], zero-initialised by the caller.
 // mode 0: plain, 1: also dres (= masked dy, identity residual), 2: also dx2 (downsample BN branch)
 IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const float* save,

@@ -38,7 +38,7 @@ struct IGemmArgs {
     const bf16_t* Wk;  // [Nout][ldb] bf16
     void* Y;           // output NHWC, channel stride ldy
     const float* bias; // [Nout] or null
-    float* stats;      // [2][Nout] (sum, sumsq) or null, fp32 atomics
+    float* stats;      // [STAT_SLOTS][2][Nout] (sum, sumsq) slab or null, fp32 atomics
     int N, H, W, C;
     int OH, OW, M;     // row grid, M = N*OH*OW
     int Nout, ldb;
@@ -51,6 +51,7 @@ struct IGemmArgs {
 #define IG_OUT_F32 1
 #define IG_RELU 2
 #define IG_STEM 4
+#define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 namespace {
 
@@ -265,8 +266,16 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
         }
     }
     if (a.stats) {
+        // Every block adds into the SAME 2*Nout words, so contention, not bytes,
+        // bounds this epilogue (MI355X_MICROARCH.md "Global float atomics":
+        // one hot row is ~14x slower). Spread the adds over STAT_SLOTS copies
+        // (slot = block id mod 32, consecutive blocks land on different XCDs)
+        // and issue one 16-lane instruction per 16 consecutive channels;
+        // imk_bn_stats_finalize folds the slots.
+        float* st = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout;
 #pragma unroll
-        for (int i = 0; i < FN; ++i)
+        for (int i = 0; i < FN; ++i) {
+            float v1 = 0.f, v2 = 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float x1 = s1[i][r], x2 = s2[i][r];
@@ -275,12 +284,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
                     x1 += __shfl_xor(x1, o, 64);
                     x2 += __shfl_xor(x2, o, 64);
                 }
-                const int n = nb + i * 16 + r;
-                if ((lane & 15) == 0 && n < a.Nout) {
-                    atomicAdd(a.stats + n, x1);
-                    atomicAdd(a.stats + a.Nout + n, x2);
+                if ((lane & 15) == r) {
+                    v1 = x1;
+                    v2 = x2;
                 }
             }
+            const int n = nb + i * 16 + (lane & 15);
+            if ((lane & 15) < 4 && n < a.Nout) {
+                atomicAdd(st + n, v1);
+                atomicAdd(st + a.Nout + n, v2);
+            }
+        }
     }
 }
 

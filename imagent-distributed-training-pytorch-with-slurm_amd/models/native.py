@@ -95,19 +95,21 @@ class NativeState:
     def _bind_workspace(self):
         bns: List[BatchNorm2d] = self.model.batchnorms()
         sizes = [bn.num_features for bn in bns]
-        per = [2 * c + 3 * c for c in sizes]           # stats + scratch (zeroed)
+        S = _lib.STAT_SLOTS
+        per = [(2 * S + 3) * c for c in sizes]          # stats slab + bwd scratch (zeroed)
         self.zero_ws = torch.zeros(sum(per), dtype=torch.float32, device=self.device)
-        self.save_ws = torch.zeros(sum(2 * c for c in sizes), dtype=torch.float32, device=self.device)
+        self.save_ws = torch.zeros(sum(4 * c for c in sizes), dtype=torch.float32, device=self.device)
         o = so = 0
         descs = (_lib.RunDesc * len(bns))()
         for i, bn in enumerate(bns):
             c = bn.num_features
-            stats = self.zero_ws[o:o + 2 * c]
-            scratch = self.zero_ws[o + 2 * c:o + 5 * c]
-            save = self.save_ws[so:so + 2 * c]
-            bn.work = BNWork(stats, None, save, None, scratch)
-            o += 5 * c
-            so += 2 * c
+            slab = self.zero_ws[o:o + 2 * S * c].view(S, 2, c)
+            scratch = self.zero_ws[o + 2 * S * c:o + (2 * S + 3) * c]
+            stats = self.save_ws[so:so + 2 * c]
+            save = self.save_ws[so + 2 * c:so + 4 * c]
+            bn.work = BNWork(slab, stats, save, scratch)
+            o += (2 * S + 3) * c
+            so += 4 * c
             d = descs[i]
             d.sums, d.rmean, d.rvar = stats.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr()
             d.nbt = bn.num_batches_tracked.data_ptr()
@@ -144,7 +146,7 @@ def bind_native(model: ResNet, device, order: Optional[Sequence[int]] = None) ->
 
 def _conv(x, conv: Conv2d, bn: Optional[BatchNorm2d], train: bool):
     if train:
-        return ConvFn.apply(x, conv.weight, conv, bn.work.stats if bn is not None else None)
+        return ConvFn.apply(x, conv.weight, conv, bn.work.slab if bn is not None else None)
     return igemm_fwd(x, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw,
                      stem=getattr(conv, "stem", False))
 

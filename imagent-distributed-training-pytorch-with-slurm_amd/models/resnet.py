@@ -97,10 +97,12 @@ class Linear(nn.Module):
 class BNWork:
     """Per-BN device workspace (views into one arena zeroed once per step)."""
 
-    __slots__ = ("stats", "stats_ds", "save", "save2", "scratch")
+    __slots__ = ("slab", "stats", "save", "scratch")
 
-    def __init__(self, stats, stats_ds, save, save2, scratch):
-        self.stats, self.stats_ds, self.save, self.save2, self.scratch = stats, stats_ds, save, save2, scratch
+    def __init__(self, slab, stats, save, scratch):
+        # slab [STAT_SLOTS, 2, C]: conv-epilogue (sum, sumsq) partials (zeroed per step)
+        # stats [2, C]: folded sums; save [2, C]: (mean, invstd); scratch [3, C]: bwd sums
+        self.slab, self.stats, self.save, self.scratch = slab, stats, save, scratch
 
 
 # --------------------------------------------------------------------------

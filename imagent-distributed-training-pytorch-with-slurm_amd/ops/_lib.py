@@ -123,6 +123,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32,
                            i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
+            "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_avgpool_fwd": [vp, vp, i32, i32, i32, vp],
@@ -181,6 +182,9 @@ def _declare(name: str, lib) -> None:
         lib.imr_tracker_last_order.restype = i32
         lib.imr_tracker_iterations.argtypes = [vp]
         lib.imr_tracker_iterations.restype = C.c_int64
+
+
+STAT_SLOTS = 32  # conv epilogue statistics slab depth (csrc/kernels/conv_igemm.hip)
 
 
 def ptr(t) -> int:

@@ -31,6 +31,13 @@ def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma
         _lib.stream_ptr()), "bn fwd")
 
 
+def stats_finalize(work) -> None:
+    """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab into ``work.stats`` [2, C]."""
+    S, _, C = work.slab.shape
+    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.stats.data_ptr(), S, C,
+                                                    _lib.stream_ptr()), "bn stats finalize")
+
+
 class BNActFn(torch.autograd.Function):
     """y = act(bn(x) [+ res | + bn2(x2)]); gamma/beta grads go to the arena.
 
@@ -41,6 +48,9 @@ class BNActFn(torch.autograd.Function):
     def forward(ctx, x, x2, bn, bn2, mode, relu):
         y = torch.empty_like(x)
         w, w2 = bn.work, (bn2.work if bn2 is not None else None)
+        stats_finalize(w)
+        if w2 is not None:
+            stats_finalize(w2)
         bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
                       stats2=w2.stats if w2 is not None else None,
                       gamma2=bn2.weight if bn2 is not None else None,

@@ -82,7 +82,7 @@ def main():
         wt = w.permute(3, 1, 2, 0).contiguous() if not stem else None
         dy = torch.randn(B, OH, OH, Co, device=dev).to(torch.bfloat16)
         dw = torch.zeros(Co, k, 32, device=dev) if stem else torch.zeros(Co, k, k, Cin, device=dev)
-        stats = torch.zeros(2, Co, device=dev)
+        stats = torch.zeros(32, 2, Co, device=dev)
         flops = 2.0 * B * OH * OH * Co * k * k * Ci
         t_f = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, stem=stem))
         t_d = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k)) if not stem else 0.0

@@ -56,8 +56,9 @@ def test_conv_fwd_dgrad_wgrad(shape):
     g = bf(torch.randn_like(yr))
     yr.backward(g.float())
 
-    stats = torch.zeros(2, Co, device=DEV)
-    y = igemm_fwd(nhwc(x), nhwc(w), s, p, k, k, stats=stats)
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(nhwc(x), nhwc(w), s, p, k, k, stats=slab)
+    stats = slab.sum(0)
     assert rel(nchw(y), yr) < 1e-2
     # epilogue BN statistics of the bf16 output
     yb = nchw(y).float()
@@ -92,8 +93,9 @@ def test_stem_row_segment_conv():
     x4[..., :3] = nhwc(x3)
     wrow = torch.zeros(Co, 7, 32, device=DEV, dtype=torch.bfloat16)
     wrow[:, :, :28].view(Co, 7, 7, 4)[..., :3] = w3.permute(0, 2, 3, 1)
-    stats = torch.zeros(2, Co, device=DEV)
-    y = igemm_fwd(x4, wrow, 2, 3, 7, 7, stats=stats, stem=True)
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(x4, wrow, 2, 3, 7, 7, stats=slab, stem=True)
+    stats = slab.sum(0)
     assert rel(nchw(y), yr) < 1e-2
     assert rel(stats[0], nchw(y).float().sum((0, 2, 3))) < 1e-3
     dw = torch.zeros(Co, 7, 32, device=DEV)
@@ -136,8 +138,10 @@ def test_bn_fwd_bwd(mode, C):
         m.weight.grad = torch.zeros_like(m.weight)
         m.bias.grad = torch.zeros_like(m.bias)
     for m, t in ((bn, x), (bn2, x2)):
-        st = torch.stack([t.float().sum((0, 1, 2)), (t.float() ** 2).sum((0, 1, 2))])
-        m.work = BNWork(st, None, torch.zeros(2, C, device=DEV), None, torch.zeros(3, C, device=DEV))
+        slab = torch.zeros(32, 2, C, device=DEV)
+        slab[3] = torch.stack([t.float().sum((0, 1, 2)), (t.float() ** 2).sum((0, 1, 2))])
+        m.work = BNWork(slab, torch.zeros(2, C, device=DEV), torch.zeros(2, C, device=DEV),
+                        torch.zeros(3, C, device=DEV))
     xa = x.clone().requires_grad_(True)
     x2a = x2.clone().requires_grad_(True)
     y = BNActFn.apply(xa, x2a if mode else None, bn, bn2 if mode == 2 else None, mode, True)
