@@ -5,15 +5,18 @@
 // (reference model at /root/reference/imagenet.py:312).
 //
 // Statistics: the per-channel (sum, sum of squares) of the BN input come from
-// the producing conv's epilogue (conv_igemm.hip, fp32 atomics), so the forward
-// is ONE streaming pass: read x (+ residual), write y.
+// the producing conv's epilogue (conv_igemm.hip, 32-slot fp32 slab folded by
+// imk_bn_stats_finalize), so the forward is ONE streaming pass: read x
+// (+ residual), write y.
 // Semantics follow nn.BatchNorm2d: biased variance to normalise, unbiased
 // variance into running_var, momentum 0.1, eps 1e-5, num_batches_tracked++.
 //
-// Backward is two streaming passes (reduce -> apply). The ReLU mask is taken
-// from the saved output y (y > 0), the residual gradient is the masked
-// upstream gradient. dgamma/dbeta are accumulated (fp32 atomics) straight into
-// the parameters' slots of the flat gradient arena.
+// Backward is two streaming passes (reduce -> apply). The ReLU mask:
+//  * plain BN+ReLU (mode 0): recomputed from x as fma(x, sc, sh) > 0 - the
+//    output y is never re-read (2 of the 6-8 bytes per element saved per pass);
+//  * BN + residual (+ReLU) (modes 1/2): taken from the saved output y > 0.
+// dgamma/dbeta are accumulated straight into the parameters' slots of the flat
+// gradient arena.
 //
 // Layout: rows r = (n, h, w), C channels contiguous; each thread owns one
 // 16-B chunk (8 channels) of a row -> per-thread channel constants live in
@@ -102,7 +105,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
         const size_t off = (size_t)r * C + c0;
         Vec8 v = ld8(x + off);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v.v[i] = v.v[i] * sc[i] + sh[i];
+        for (int i = 0; i < 8; ++i) v.v[i] = fmaf(v.v[i], sc[i], sh[i]);
         if (MODE == 1) {
             const Vec8 s = ld8(x2 + off);
 #pragma unroll
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
         } else if (MODE == 2) {
             const Vec8 s = ld8(x2 + off);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v.v[i] += s.v[i] * sc2[i] + sh2[i];
+            for (int i = 0; i < 8; ++i) v.v[i] += fmaf(s.v[i], sc2[i], sh2[i]);
         }
         if (RELU) {
 #pragma unroll
@@ -120,9 +123,8 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     }
 }
 
-// running stats update + num_batches_tracked (one tiny launch per BN layer
-// would be wasteful: all layers of a step are updated by ONE launch over a
-// descriptor table, see imk_bn_running_update)
+// running stats update + num_batches_tracked: all layers of a step are updated
+// by ONE launch over a descriptor table (imk_bn_running_update)
 struct RunDesc {
     const float* sums;
     float* rmean;
@@ -143,25 +145,60 @@ __global__ void bn_running_kernel(const RunDesc* __restrict__ d, int n) {
     if (threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
+// Fold the conv epilogue's [S][2][C] statistics slab into [2][C] sums.
+__global__ __launch_bounds__(64) void stats_finalize_kernel(const float* __restrict__ slab,
+                                                            float* __restrict__ out, int S, int n2c) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n2c) return;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int k = 0; k < S; ++k) s[k & 3] += slab[(size_t)k * n2c + i];
+    out[i] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
 // ---------------------------------------------------------------- backward
-// g = dy * (y > 0)   (RELU) ; per-channel sums  Sg = sum g,  Sgx = sum g * xhat
-// (MODE 2 also Sgx2 over the downsample branch x2 with its own statistics),
-// written to a zeroed fp32 scratch [3][C] with one atomic per channel per block.
-template <bool RELU, int MODE>
+// MASK 0: no ReLU; 1: ReLU mask from the saved output y; 2: from x (mode 0 only:
+// y = relu(fma(x, sc, sh)) with the forward's sc = rstd*gamma, sh = beta - mean*sc)
+template <int MASK>
+__device__ __forceinline__ void relu_mask(Vec8& g, const bf16_t* y, const Vec8& xv, const float* sc,
+                                          const float* sh) {
+    if (MASK == 1) {
+        const u32x4 yw = *reinterpret_cast<const u32x4*>(y);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
+            if (!(hi_bf(yw[i]) > 0.f)) g.v[2 * i + 1] = 0.f;
+        }
+    } else if (MASK == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (!(fmaf(xv.v[i], sc[i], sh[i]) > 0.f)) g.v[i] = 0.f;
+    }
+}
+
+// per-channel sums  Sg = sum g,  Sgx = sum g * xhat  (MODE 2 also Sgx2 over
+// the downsample branch x2) into a zeroed fp32 scratch [3][C], one atomic per
+// channel per block.
+template <int MASK, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ save, const bf16_t* __restrict__ x2, const float* __restrict__ save2,
-    float* __restrict__ scratch, long R, int C) {
+    const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const bf16_t* __restrict__ x2, const float* __restrict__ save2, float* __restrict__ scratch, long R,
+    int C) {
     __shared__ float red[2048];  // [rpb][C], rpb*C == 2048
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
     const bool active = tid < rpb * cpr;
     const int ch = tid % cpr, c0 = ch * 8, rsub = tid / cpr;
-    float mean[8], rstd[8], m2[8], r2[8];
+    float mean[8], rstd[8], m2[8], r2[8], sc[8], sh[8];
     float acc[3][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         mean[i] = save[c0 + i];
         rstd[i] = save[C + c0 + i];
+        if (MASK == 2) {
+            sc[i] = rstd[i] * gamma[c0 + i];
+            sh[i] = beta[c0 + i] - mean[i] * sc[i];
+        }
         if (MODE == 2) {
             m2[i] = save2[c0 + i];
             r2[i] = save2[C + c0 + i];
@@ -172,15 +209,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         for (long r = (long)blockIdx.x * rpb + rsub; r < R; r += (long)gridDim.x * rpb) {
             const size_t off = (size_t)r * C + c0;
             Vec8 g = ld8(dy + off);
-            if (RELU) {
-                const u32x4 yw = *reinterpret_cast<const u32x4*>(y + off);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
-                    if (!(hi_bf(yw[i]) > 0.f)) g.v[2 * i + 1] = 0.f;
-                }
-            }
             const Vec8 xv = ld8(x + off);
+            relu_mask<MASK>(g, y + off, xv, sc, sh);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 acc[0][i] += g.v[i] * (xv.v[i] - mean[i]) * rstd[i];
@@ -214,14 +244,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // dx = gamma*rstd*(g - Sg/R - xhat*Sgx/R); MODE 1 also writes the residual
 // gradient g, MODE 2 the downsample-branch input gradient. Block 0 also adds
 // the sums into the arena slots of dgamma/dbeta (+= : gradient accumulation).
-template <bool RELU, int MODE>
+template <int MASK, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ scratch,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, const bf16_t* __restrict__ x2,
-    const float* __restrict__ save2, const float* __restrict__ gamma2, bf16_t* __restrict__ dx2,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dgamma2,
-    float* __restrict__ dbeta2, long R, int C, float inv_cnt) {
+    const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ scratch, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+    const bf16_t* __restrict__ x2, const float* __restrict__ save2, const float* __restrict__ gamma2,
+    bf16_t* __restrict__ dx2, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt) {
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
@@ -235,13 +265,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
     if (tid >= rpb * cpr) return;
     const int ch = tid % cpr, c0 = ch * 8;
-    float k1[8], k2[8], k3[8], mean[8], q1[8], q2[8], q3[8], m2[8];
+    float k1[8], k2[8], k3[8], mean[8], q1[8], q2[8], q3[8], m2[8], sc[8], sh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int c = c0 + i;
         mean[i] = save[c];
         const float rstd = save[C + c];
         const float gr = gamma[c] * rstd;
+        if (MASK == 2) {
+            sc[i] = gr;
+            sh[i] = beta[c] - mean[i] * gr;
+        }
         k1[i] = gr;
         k2[i] = -gr * inv_cnt * scratch[C + c];
         k3[i] = -gr * inv_cnt * scratch[c] * rstd;
@@ -257,15 +291,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     for (long r = (long)blockIdx.x * rpb + tid / cpr; r < R; r += (long)gridDim.x * rpb) {
         const size_t off = (size_t)r * C + c0;
         Vec8 g = ld8(dy + off);
-        if (RELU) {
-            const u32x4 yw = *reinterpret_cast<const u32x4*>(y + off);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
-                if (!(hi_bf(yw[i]) > 0.f)) g.v[2 * i + 1] = 0.f;
-            }
-        }
         const Vec8 xv = ld8(x + off);
+        relu_mask<MASK>(g, y + off, xv, sc, sh);
         Vec8 o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g.v[i] + k2[i] + k3[i] * (xv.v[i] - mean[i]);
@@ -320,21 +347,9 @@ IMK_EXPORT int imk_bn_running_update(const void* descs, int n, void* stream) {
 
 IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
 
-// Fold the conv epilogue's [S][2][C] statistics slab into [2][C] sums.
-namespace {
-__global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __restrict__ slab,
-                                                             float* __restrict__ out, int S, int n2c) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n2c) return;
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += slab[(size_t)k * n2c + i];
-    out[i] = s;
-}
-}  // namespace
-
 IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C, void* stream) {
     const int n2c = 2 * C;
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2c + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2c + 63) / 64), dim3(64), 0, (hipStream_t)stream,
                        slab, out, S, n2c);
     IMK_CHECK_LAUNCH();
     return 0;
@@ -342,31 +357,34 @@ IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C
 
 // scratch: fp32 [3][C], zero-initialised by the caller.
 // mode 0: plain, 1: also dres (= masked dy, identity residual), 2: also dx2 (downsample BN branch)
+// relu: 0 none, 1 mask from y, 2 mask from x (mode 0 only; needs gamma/beta/save as in forward)
 IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const float* save,
-                          const float* gamma, const void* x2, const float* save2,
+                          const float* gamma, const float* beta, const void* x2, const float* save2,
                           const float* gamma2, float* scratch, void* dx, void* dres, void* dx2,
                           float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
                           float* dbeta2_acc, long R, int C, int mode, int relu, void* stream) {
     if (C % 8 || C > 2048) return -100;
+    if (relu == 2 && mode != 0) return -101;
     hipStream_t st = (hipStream_t)stream;
     const int grid = grid_for(R, C);
     const int rgrid = grid < 1024 ? grid : 1024;
-#define LR(RL, M)                                                                                  \
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<RL, M>), dim3(rgrid), dim3(256), 0, st,               \
-                       (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, save, (const bf16_t*)x2, \
-                       save2, scratch, R, C)
-    if (relu) { if (mode == 2) LR(true, 2); else LR(true, 0); }
-    else { if (mode == 2) LR(false, 2); else LR(false, 0); }
+#define LR(MK, M)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK, M>), dim3(rgrid), dim3(256), 0, st,               \
+                       (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta,    \
+                       (const bf16_t*)x2, save2, scratch, R, C)
+    if (mode == 2) { if (relu) LR(1, 2); else LR(0, 2); }
+    else { if (relu == 2) LR(2, 0); else if (relu) LR(1, 0); else LR(0, 0); }
 #undef LR
     IMK_CHECK_LAUNCH();
     const float inv_cnt = 1.f / (float)R;
-#define LA(RL, M)                                                                                  \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
-                       (const bf16_t*)y, (const bf16_t*)x, save, gamma, scratch, (bf16_t*)dx,        \
+#define LA(MK, M)                                                                                  \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
+                       (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, scratch, (bf16_t*)dx,  \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
                        dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
-    if (relu) { if (mode == 0) LA(true, 0); else if (mode == 1) LA(true, 1); else LA(true, 2); }
-    else { if (mode == 0) LA(false, 0); else if (mode == 1) LA(false, 1); else LA(false, 2); }
+    if (mode == 0) { if (relu == 2) LA(2, 0); else if (relu) LA(1, 0); else LA(0, 0); }
+    else if (mode == 1) { if (relu) LA(1, 1); else LA(0, 1); }
+    else { if (relu) LA(1, 2); else LA(0, 2); }
 #undef LA
     IMK_CHECK_LAUNCH();
     return 0;

@@ -367,7 +367,12 @@ int launch(const IGemmArgs& a, hipStream_t st) {
             cus = 256;
         resident = per_cu * cus;
     }
-    const int grid = ntiles < resident ? ntiles : resident;
+    // persistent only where it pays: tiles with few K-stages (memory-bound 1x1
+    // convs) overlap the next tile's loads with this tile's epilogue; long-K
+    // tiles keep one tile per block (the hardware refills CUs without a tail)
+    const int K = MD == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
+    const int nk = (K + BK - 1) / BK;
+    const int grid = (nk > 4 || ntiles < resident) ? ntiles : resident;
     hipLaunchKernelGGL((igemm_kernel<BM, BN, WN, MD>), dim3(grid), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;

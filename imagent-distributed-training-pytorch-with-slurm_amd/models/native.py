@@ -16,6 +16,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..ops import _lib
+from ..ops.block import BlockFn
 from ..ops.bn import BNActFn, bn_eval, running_update
 from ..ops.conv import ConvFn, LinearFn, igemm_fwd
 from ..ops.misc import AvgPoolFn, MaxPoolFn, TransposePlan, maxpool_eval
@@ -35,6 +36,9 @@ class NativeState:
         named = list(model.named_parameters())
         self.arena = ParamArena(named, self.device, order=order, with_shadow=True)
         self.model = model
+        # one autograd node per residual block with a hand-scheduled backward
+        # (ops/block.py); False = per-op autograd nodes (used to cross-check)
+        self.fused_blocks = True
         self._bind_shadows()
         self._bind_workspace()
 
@@ -172,6 +176,10 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     y = _bn(y, model.bn1, True, train)
     y = MaxPoolFn.apply(y, 3, 2, 1) if train else maxpool_eval(y, 3, 2, 1)
     for b in model.blocks():
+        if train and st.fused_blocks:
+            y = BlockFn.apply(y, b)
+            rows.extend(b._bn_rows)
+            continue
         idt = y
         pairs = b.convs_bns()
         out = y

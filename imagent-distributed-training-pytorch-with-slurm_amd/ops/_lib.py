@@ -120,8 +120,7 @@ def _declare(name: str, lib) -> None:
             "imk_conv_igemm": [C.POINTER(IGemmArgs), i32, vp],
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp],
-            "imk_bn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32,
-                           i32, vp],
+            "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],

@@ -1,8 +1,9 @@
 """BatchNorm(+residual add)(+ReLU) on the fused HIP kernels (NHWC bf16).
 
-Training-mode statistics arrive from the producing conv's epilogue as
-per-channel (sum, sum of squares) in fp32 (``stats``), so the forward is one
-streaming pass. ``save`` receives (mean, invstd) for the backward.
+Training-mode statistics arrive from the producing conv's epilogue as a
+``[STAT_SLOTS, 2, C]`` slab of fp32 partial (sum, sum of squares), folded by
+one tiny launch, so the forward is one streaming pass. ``save`` receives
+(mean, invstd) for the backward.
 
 Three forms cover torchvision's blocks (reference model: ``imagenet.py:312``):
   mode 0  y = act(bn(x))                       (conv1/conv2 of a block, stem)
@@ -12,12 +13,19 @@ Three forms cover torchvision's blocks (reference model: ``imagenet.py:312``):
 
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
 from . import _lib
 from .grad_sink import notify_ready
+
+
+def stats_finalize(work) -> None:
+    """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab into ``work.stats`` [2, C]."""
+    S, _, C = work.slab.shape
+    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.stats.data_ptr(), S, C,
+                                                    _lib.stream_ptr()), "bn stats finalize")
 
 
 def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
@@ -31,61 +39,66 @@ def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma
         _lib.stream_ptr()), "bn fwd")
 
 
-def stats_finalize(work) -> None:
-    """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab into ``work.stats`` [2, C]."""
-    S, _, C = work.slab.shape
-    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.stats.data_ptr(), S, C,
-                                                    _lib.stream_ptr()), "bn stats finalize")
+def bn_act_forward(x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2, mode: int, relu: bool) -> torch.Tensor:
+    """Training-mode forward (no autograd): statistics from ``bn.work.slab``."""
+    y = torch.empty_like(x)
+    w, w2 = bn.work, (bn2.work if bn2 is not None else None)
+    stats_finalize(w)
+    if w2 is not None:
+        stats_finalize(w2)
+    bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
+                  stats2=w2.stats if w2 is not None else None,
+                  gamma2=bn2.weight if bn2 is not None else None,
+                  beta2=bn2.bias if bn2 is not None else None,
+                  save2=w2.save if w2 is not None else None, mode=mode, relu=relu, eps=bn.eps)
+    return y
+
+
+def bn_act_backward(dy: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor], y: Optional[torch.Tensor],
+                    bn, bn2, mode: int, relu: bool,
+                    dres: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Returns (dx, dres | dx2). dgamma/dbeta land in the gradient arena and the
+    reducer is notified. Mode 0 + ReLU recomputes the mask from x (y unused)."""
+    w = bn.work
+    C = x.shape[-1]
+    R = x.numel() // C
+    dx = torch.empty_like(x)
+    if mode == 1 and dres is None:
+        dres = torch.empty_like(x)
+    dx2 = torch.empty_like(x2) if mode == 2 else None
+    rmode = (2 if mode == 0 else 1) if relu else 0
+    _lib.check(_lib.kernels().imk_bn_bwd(
+        dy.data_ptr(), y.data_ptr() if rmode == 1 else 0, x.data_ptr(), w.save.data_ptr(),
+        bn.weight.data_ptr(), bn.bias.data_ptr(), _lib.ptr(x2) if mode == 2 else 0,
+        bn2.work.save.data_ptr() if mode == 2 else 0,
+        bn2.weight.data_ptr() if mode == 2 else 0, w.scratch.data_ptr(), dx.data_ptr(),
+        _lib.ptr(dres) if mode == 1 else 0, _lib.ptr(dx2), bn.weight.grad.data_ptr(),
+        bn.bias.grad.data_ptr(), bn2.weight.grad.data_ptr() if mode == 2 else 0,
+        bn2.bias.grad.data_ptr() if mode == 2 else 0,
+        R, C, mode, rmode, _lib.stream_ptr()), "bn bwd")
+    notify_ready(bn.weight)
+    notify_ready(bn.bias)
+    if mode == 2:
+        notify_ready(bn2.weight)
+        notify_ready(bn2.bias)
+    return dx, (dres if mode == 1 else dx2)
 
 
 class BNActFn(torch.autograd.Function):
-    """y = act(bn(x) [+ res | + bn2(x2)]); gamma/beta grads go to the arena.
-
-    ``bn.work`` holds the conv-epilogue statistics (``stats``), the saved
-    (mean, invstd) (``save``) and the zeroed backward scratch."""
+    """y = act(bn(x) [+ res | + bn2(x2)]) as an autograd node (stem, tests)."""
 
     @staticmethod
     def forward(ctx, x, x2, bn, bn2, mode, relu):
-        y = torch.empty_like(x)
-        w, w2 = bn.work, (bn2.work if bn2 is not None else None)
-        stats_finalize(w)
-        if w2 is not None:
-            stats_finalize(w2)
-        bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
-                      stats2=w2.stats if w2 is not None else None,
-                      gamma2=bn2.weight if bn2 is not None else None,
-                      beta2=bn2.bias if bn2 is not None else None,
-                      save2=w2.save if w2 is not None else None, mode=mode, relu=relu, eps=bn.eps)
+        y = bn_act_forward(x, x2, bn, bn2, mode, relu)
         ctx.bn, ctx.bn2, ctx.mode, ctx.relu = bn, bn2, mode, relu
-        ctx.save_for_backward(x, x2 if mode == 2 else None, y)
+        ctx.save_for_backward(x, x2 if mode == 2 else None, y if mode != 0 else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, x2, y = ctx.saved_tensors
-        bn, bn2, mode = ctx.bn, ctx.bn2, ctx.mode
-        w = bn.work
-        dy = dy.contiguous()
-        C = x.shape[-1]
-        R = x.numel() // C
-        dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if mode == 1 else None
-        dx2 = torch.empty_like(x2) if mode == 2 else None
-        _lib.check(_lib.kernels().imk_bn_bwd(
-            dy.data_ptr(), y.data_ptr() if ctx.relu else 0, x.data_ptr(), w.save.data_ptr(),
-            bn.weight.data_ptr(), _lib.ptr(x2) if mode == 2 else 0,
-            bn2.work.save.data_ptr() if mode == 2 else 0,
-            bn2.weight.data_ptr() if mode == 2 else 0, w.scratch.data_ptr(), dx.data_ptr(),
-            _lib.ptr(dres), _lib.ptr(dx2), bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
-            bn2.weight.grad.data_ptr() if mode == 2 else 0,
-            bn2.bias.grad.data_ptr() if mode == 2 else 0,
-            R, C, mode, 1 if ctx.relu else 0, _lib.stream_ptr()), "bn bwd")
-        notify_ready(bn.weight)
-        notify_ready(bn.bias)
-        if mode == 2:
-            notify_ready(bn2.weight)
-            notify_ready(bn2.bias)
-        return dx, (dres if mode == 1 else dx2), None, None, None, None
+        dx, dsecond = bn_act_backward(dy.contiguous(), x, x2, y, ctx.bn, ctx.bn2, ctx.mode, ctx.relu)
+        return dx, dsecond, None, None, None, None
 
 
 def bn_eval(x, bn, relu, x2=None, bn2=None, mode=0):

@@ -77,13 +77,17 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
 
 
 def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
-                KH: int, KW: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dx[N,H,W,Ci] from dy[N,OH,OW,Co] and wt[Ci,KH,KW,Co].
+                KH: int, KW: int, out: Optional[torch.Tensor] = None,
+                accumulate: bool = False) -> torch.Tensor:
+    """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci,KH,KW,Co]).
 
     Stride 1: one gather-GEMM launch with the taps mirrored.
     Stride s: s*s launches, one per output parity class, each touching only
     the taps that hit it (sub-pixel decomposition: no multiply-by-zero work).
+    ``accumulate``: the epilogue adds into ``out`` (fuses a residual-branch
+    gradient sum into the store instead of a separate add kernel).
     """
+    assert not accumulate or out is not None
     N, OH, OW, Co = dy.shape
     Ci = wt.shape[0]
     H, W = in_hw
@@ -102,6 +106,8 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             kw0 = (pw + pad) % S
             nth = max(0, (KH - kh0 + S - 1) // S)
             ntw = max(0, (KW - kw0 + S - 1) // S)
+            if accumulate and (nth == 0 or ntw == 0):
+                continue  # no tap reaches this parity class: nothing to add
             a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
                            KH * KW * Co, 1)
             a.nth, a.ntw = nth, ntw
@@ -109,7 +115,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = 0
+            a.flags = 8 if accumulate else 0
             _lib.check(k.imk_conv_igemm(C.byref(a), 0, st), "conv dgrad")
     return out
 
@@ -167,16 +173,22 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = igemm_dgrad(dy, mod.wt_bf16, (x.shape[1], x.shape[2]), mod.stride, mod.padding, mod.kh,
                              mod.kw)
-        gp = getattr(mod, "grad_pad", None)
-        if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
-            gp.zero_()
-            igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw, stem=True)
-            real = gp[:, :, : mod.kw * 4].view(gp.shape[0], mod.kh, mod.kw, 4)[..., : mod.in_channels]
-            mod.weight.grad.permute(0, 2, 3, 1).add_(real)
-        else:
-            igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw)
-        notify_ready(mod.weight)
+        conv_wgrad(mod, dy, x)
         return dx, None, None, None
+
+
+def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
+    """Accumulate a Conv2d module's weight gradient into its arena slot and
+    signal the bucketed reducer."""
+    gp = getattr(mod, "grad_pad", None)
+    if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
+        gp.zero_()
+        igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw, stem=True)
+        real = gp[:, :, : mod.kw * 4].view(gp.shape[0], mod.kh, mod.kw, 4)[..., : mod.in_channels]
+        mod.weight.grad.permute(0, 2, 3, 1).add_(real)
+    else:
+        igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw)
+    notify_ready(mod.weight)
 
 
 class LinearFn(torch.autograd.Function):

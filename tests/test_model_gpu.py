@@ -29,8 +29,8 @@ def _grads(model, x, lab, autocast=False):
     return logits.float(), {n: p.grad.float().clone() for n, p in model.named_parameters()}
 
 
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_hip_vs_torch_forward_backward(arch):
+@pytest.mark.parametrize("arch,fused", [("resnet18", True), ("resnet50", True), ("resnet50", False)])
+def test_hip_vs_torch_forward_backward(arch, fused):
     from imagent_amd.models import resnet
     from imagent_amd.models.native import bind_native
     from imagent_amd.ops.misc import normalize_u8
@@ -38,6 +38,7 @@ def test_hip_vs_torch_forward_backward(arch):
     ref = resnet.build(arch, num_classes=1000).to(DEV)
     model = copy.deepcopy(ref)
     st = bind_native(model, DEV)
+    st.fused_blocks = fused
     with torch.no_grad():  # the oracle sees exactly the bf16-rounded weights the kernels use
         for p_ref, p in zip(ref.parameters(), model.parameters()):
             p_ref.copy_(p.to(torch.bfloat16).float())
