@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--miopen", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
     dev = "cuda"
@@ -71,6 +72,8 @@ def main():
     print(f"{'Ci':>5} {'H':>4} {'Co':>5} k s | cnt | {'fwd us':>8} {'TF':>6} {'roof':>6} | {'dgrad':>8} {'TF':>6} | "
           f"{'wgrad':>8} {'TF':>6}" + (" | miopen fwd" if a.miopen else ""))
     for (Ci, H, Co, k, s, p), cnt in shapes(a.arch, a.batch, a.size).items():
+        if a.only and tuple(int(v) for v in a.only.split(",")) != (Ci, H, Co, k, s):
+            continue
         stem = Ci == 3
         Cin = 4 if stem else Ci
         B = a.batch
