@@ -31,7 +31,7 @@
 // small-K layers (ResNet 1x1 convs have 1-4 K-stages per tile), where a
 // one-tile-per-block grid serialised load -> compute -> store.
 // 256 threads = 4 waves; block tile BM pixels x BN channels; BK = 64; LDS
-// double buffer, rows padded by 16 B. MFMA v_mfma_f32_16x16x32_bf16 with the
+// double buffer, 128-B rows with an XOR chunk swizzle (conflict-free reads). MFMA v_mfma_f32_16x16x32_bf16 with the
 // WEIGHTS as the A operand and the pixels as the B operand, so each lane's
 // accumulator holds 4 consecutive output CHANNELS of one pixel: 8-byte NHWC
 // stores with no LDS pass, and BN statistics (sum, sum of squares) reduce over
@@ -65,7 +65,7 @@ struct IGemmArgs {
 namespace {
 
 constexpr int BK = 64;
-constexpr int LDK = BK + 8;  // padded row (elements): 144 B
+constexpr int LDK = BK;  // 128-B rows, 16-B chunks XOR-swizzled by (row & 7): conflict-free ds_read_b128
 
 template <int BM, int BN, int WN, int MODE>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
@@ -178,10 +178,10 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
         bf16_t* dw = sW + buf * BN * LDK;
 #pragma unroll
         for (int i = 0; i < A_CH; ++i)
-            *reinterpret_cast<u32x4*>(dx + ((tid >> 3) + 32 * i) * LDK + col8 * 8) = rx[i];
+            *reinterpret_cast<u32x4*>(dx + ((tid >> 3) + 32 * i) * LDK + ((col8 ^ ((tid >> 3) & 7)) * 8)) = rx[i];
 #pragma unroll
         for (int j = 0; j < B_CH; ++j)
-            *reinterpret_cast<u32x4*>(dw + ((tid >> 3) + 32 * j) * LDK + col8 * 8) = rw[j];
+            *reinterpret_cast<u32x4*>(dw + ((tid >> 3) + 32 * j) * LDK + ((col8 ^ ((tid >> 3) & 7)) * 8)) = rw[j];
     };
 
     f32x4 acc[FN][FM];
@@ -305,7 +305,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     load_stage(0);
     store_stage(0);
     __syncthreads();
-    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    const int fr = lane & 15;
+    // physical chunk of logical chunk (lane>>4) + 4*ks in a row with (row & 7) == (fr & 7)
+    const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
     int tj = 0, kt = 0;  // tile ordinal / stage within tile of stage s
     for (int s = 0; s < nstages; ++s) {
         const int buf = s & 1;
@@ -318,17 +320,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
                 load_stage(kt + 1);
             }
         }
-        const bf16_t* bx = sX + buf * BM * LDK + (wm * TM + fr) * LDK + fk;
-        const bf16_t* bw = sW + buf * BN * LDK + (wn * TN + fr) * LDK + fk;
+        const bf16_t* bx = sX + buf * BM * LDK + (wm * TM + fr) * LDK;
+        const bf16_t* bw = sW + buf * BN * LDK + (wn * TN + fr) * LDK;
 #pragma unroll
         for (int ks = 0; ks < BK / 32; ++ks) {
             bf16x8 fw[FN], fx[FM];
 #pragma unroll
             for (int i = 0; i < FN; ++i)
-                fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + ks * 32);
+                fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + (ks ? fk1 : fk0));
 #pragma unroll
             for (int j = 0; j < FM; ++j)
-                fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + ks * 32);
+                fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + (ks ? fk1 : fk0));
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll

@@ -195,6 +195,24 @@ class DataParallel(nn.Module):
             self.buckets.append((lo, hi, members))
         self.tracker = _Tracker(bucket_of, nb)
 
+    @torch.no_grad()
+    def check_consistency(self, raise_on_mismatch: bool = True) -> bool:
+        """Race / divergence detector: after identical averaged
+        gradients every rank must hold bit-identical parameters. A bucket read
+        by RCCL before its producing kernel finished, or a compute kernel
+        overwriting a bucket during its all-reduce, shows up here as a
+        checksum mismatch. Costs one tiny all-gather; call it every N steps."""
+        if self.comm.world_size <= 1:
+            return True
+        P = self.arena.P
+        sig = torch.stack([P.double().sum(), (P.double() * torch.arange(P.numel(), device=P.device,
+                                                                         dtype=torch.float64).remainder_(977)).sum()])
+        allsig = self.comm.allgather(sig)
+        ok = bool((allsig == allsig[0]).all())
+        if not ok and raise_on_mismatch:
+            raise RuntimeError(f"DataParallel: parameters diverged across ranks: {allsig.tolist()}")
+        return ok
+
     def bucket_sizes_mb(self) -> List[float]:
         return [(hi - lo) * 4 / MB for lo, hi, _ in self.buckets]
 

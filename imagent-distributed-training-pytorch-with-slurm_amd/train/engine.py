@@ -17,6 +17,7 @@ TensorBoard tags, best-model checkpoint), re-designed for MI355X:
 
 from __future__ import annotations
 
+import faulthandler
 import json
 import math
 import os
@@ -193,6 +194,9 @@ class Trainer:
                                    after_step=after, full_refresh=full,
                                    schedule_decay=a.schedule_decay)
         self.metrics = DeviceMetrics(self.device)
+        from ..utils.profiling import StepTimer
+        self.timer = StepTimer(enabled=self.device.type == "cuda")
+        self.last_step_pct = {}
         ac = None
         if self.kernels == "torch" and self.device.type == "cuda" and a.dtype == "bf16":
             ac = torch.bfloat16
@@ -238,7 +242,14 @@ class Trainer:
                 continue
             if per_iter:
                 lr = self.sched.apply(self.opt, epoch, it)
+            if a.step_timeout > 0:   # hang detector: dump every thread's stack if a step stalls
+                faulthandler.dump_traceback_later(a.step_timeout, exit=False)
+            self.timer.mark()
             self.step.train_step(micro)
+            if a.step_timeout > 0:
+                faulthandler.cancel_dump_traceback_later()
+            if a.check_consistency and (it + 1) % a.check_consistency == 0:
+                self.ddp.check_consistency()
             # one-time bucket rebuild from the observed ready order (iteration 1)
             if getattr(self.ddp, "pending_relayout", None) is not None:
                 self.opt.set_flats(self.ddp.apply_pending_relayout(self.opt.flats()))
@@ -257,11 +268,14 @@ class Trainer:
                 tlog, nlog = now, 0
             if it >= max_steps:
                 break
+        self.timer.mark()
         self._sync()
         dt = time.time() - t0
         loss, t1, t5, n = self.metrics.reduced(self.comm)
         self.last_train_images = n
         self.last_lr = lr
+        self.last_step_pct = self.timer.percentiles()
+        self.timer.events.clear()
         return loss, t1, t5, dt
 
     @torch.no_grad()
@@ -311,6 +325,12 @@ class Trainer:
                 print(f"\tTrain time: {t_train} seconds; Test time:{t_val} seconds")
                 print(f"\tThroughput: {ips:.1f} img/s (job), {ips / self.ctx.world_size:.1f} img/s/GPU",
                       flush=True)
+                if self.last_step_pct:
+                    p = self.last_step_pct
+                    print(f"\tStep time ms p50/p90/p99: {p[50]:.2f}/{p[90]:.2f}/{p[99]:.2f}", flush=True)
+                if self.device.type == "cuda":
+                    print(f"\tPeak HBM allocated: {torch.cuda.max_memory_allocated(self.device) / 2**30:.2f} GiB",
+                          flush=True)
                 if self.tb:   # imagenet.py:405-421 (lr step 0-based, quirk Q4 kept)
                     self.tb.add_scalars("Loss", {"train": tr_loss, "val": va_loss}, epoch + 1)
                     self.tb.add_scalars("Top1 accuracy", {"train": tr1, "val": va1}, epoch + 1)
