@@ -4,9 +4,9 @@
 // torchvision resnet18 (/root/reference/imagenet.py:312, forward :123,
 // backward :128).
 //
-// ONE "gather GEMM" kernel serves the forward conv, the stride-1 dgrad, each
-// parity class of a strided dgrad (sub-pixel decomposition, no wasted MACs),
-// the 7x7 stem and the FC layer (a 1x1 conv on a 1x1 image):
+// ONE "gather GEMM" formulation serves the forward conv, the stride-1 dgrad,
+// each parity class of a strided dgrad (sub-pixel decomposition, no wasted
+// MACs), the 7x7 stem and the FC layer (a 1x1 conv on a 1x1 image):
 //
 //   out[pix(m)][n] = sum_{t < ntaps, c < C} X[gather(m, t)][c] * Wk[n][wtap(t)*C + c]
 //
@@ -20,24 +20,32 @@
 //  * dgrad (s=1):  X = dY, dh0 = pad, dhs = -1, Wk = W^T[Ci][KH][KW][Co]
 //  * dgrad (s>1):  one launch per output parity (ph, pw); only the taps with
 //                  kh == (ph + pad) mod s contribute, output pixel s*oh + ph.
-//  * stem (MODE 2): C == 4, the KW taps x 4 channels of a kernel row are one
+//  * stem:         C == 4, the KW taps x 4 channels of a kernel row are one
 //                  contiguous NHWC segment -> K = KH x 32 (28 real + 4 zero).
 //
-// Structure: a PERSISTENT grid (occupancy x CUs blocks). Each block walks its
-// output tiles and their K-stages as ONE flattened sequence of stages, so the
-// register-staged global loads of stage s+1 (possibly the first stage of the
-// NEXT tile) are in flight while stage s runs its MFMAs and, at a tile's last
-// stage, its epilogue. This keeps HBM streaming for the memory-bound
-// small-K layers (ResNet 1x1 convs have 1-4 K-stages per tile), where a
-// one-tile-per-block grid serialised load -> compute -> store.
-// 256 threads = 4 waves; block tile BM pixels x BN channels; BK = 64; LDS
-// double buffer, 128-B rows with an XOR chunk swizzle (conflict-free reads). MFMA v_mfma_f32_16x16x32_bf16 with the
-// WEIGHTS as the A operand and the pixels as the B operand, so each lane's
-// accumulator holds 4 consecutive output CHANNELS of one pixel: 8-byte NHWC
-// stores with no LDS pass, and BN statistics (sum, sum of squares) reduce over
-// the 16 lanes of a row group, then go to a 32-slot slab with fp32 atomics.
-// Tiles are XCD-remapped so concurrently running channel tiles of one pixel
-// panel share an XCD's L2.
+// Two main-loop structures share one epilogue:
+//
+//  igemm_dma_kernel (every conv except the stem): operands go global -> LDS
+//    by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece = 8 tile rows per
+//    wave instruction, per-lane gather addresses, out-of-image taps read a
+//    zero line) into an NS-deep ring of 128-B-row tiles. Stage s+NS-1 is in
+//    flight while stage s computes; a counted s_waitcnt vmcnt + raw s_barrier
+//    retire one stage per iteration (cdna_hip_programming.md §5 "Pipelining
+//    across barriers"). No VGPRs, no ds_write for staging.
+//  igemm_rs_kernel (stem): register staging with 8-byte half-predicated loads.
+//
+// Both are PERSISTENT when tiles have few K-stages: a block walks its tiles
+// and their K-stages as ONE flattened stage sequence, so the next tile's loads
+// overlap this tile's epilogue (memory-bound 1x1 convs).
+// LDS tiles: 128-B rows (BK = 64 bf16) with 16-B chunks XOR-swizzled by
+// (row & 7) -> conflict-free ds_read_b128 fragment reads (swizzle applied on
+// the DMA SOURCE address, the LDS image stays lane-linear).
+// MFMA v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A operand and the
+// pixels as the B operand: each lane's accumulator holds 4 consecutive output
+// CHANNELS of one pixel -> 8-byte NHWC stores with no LDS pass; BN statistics
+// (sum, sum of squares) reduce over the 16 lanes of a row group and go to a
+// 32-slot fp32 slab. Tiles are XCD-remapped so concurrently running channel
+// tiles of one pixel panel share an XCD's L2.
 
 #include "common.h"
 
@@ -58,17 +66,310 @@ struct IGemmArgs {
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
 #define IG_RELU 2      // ReLU on the output
-#define IG_STEM 4      // stem row-segment gather (MODE 2)
+#define IG_STEM 4      // stem row-segment gather
 #define IG_ACCUM 8     // out += result (bf16 out only): fused gradient accumulation
+#define IG_REGSTAGE 16 // force the register-staged main loop (A/B testing)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
+
+__device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes
 
 namespace {
 
-constexpr int BK = 64;
-constexpr int LDK = BK;  // 128-B rows, 16-B chunks XOR-swizzled by (row & 7): conflict-free ds_read_b128
+constexpr int BK = 64;   // K elements per stage = one 128-B LDS row
+constexpr int LDK = BK;
 
+__device__ __forceinline__ void waitcnt_vm(int n) {
+    // s_waitcnt vmcnt(n) only (expcnt/lgkmcnt left at their maxima); n is a
+    // small compile-time-like value chosen by an unrolled switch at the call site
+#define WV(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+    switch (n) {
+        case 0: WV(0); break;
+        case 4: WV(4); break;
+        case 6: WV(6); break;
+        case 8: WV(8); break;
+        case 12: WV(12); break;
+        case 16: WV(16); break;
+        default: WV(0); break;
+    }
+#undef WV
+}
+
+// ------------------------------------------------------------------ epilogue
+// lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
+template <int FN, int FM>
+__device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb,
+                                              int lane, float* st) {
+    const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU, accum = a.flags & IG_ACCUM;
+    const int ohw = a.OH * a.OW;
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= a.M) continue;
+        const int img = m / ohw, rem = m - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const size_t pix = ((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int n = nb + i * 16;
+            if (n >= a.Nout) continue;
+            const bool full = n + 3 < a.Nout && (a.ldy % 4) == 0;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[i][j][r];
+                if (a.bias) v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
+            }
+            if (out_f32) {
+                float* y = reinterpret_cast<float*>(a.Y) + pix * a.ldy + n;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (relu) v[r] = fmaxf(v[r], 0.f);
+                if (full) {
+                    *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
+                } else {
+                    for (int r = 0; r < 4; ++r)
+                        if (n + r < a.Nout) y[r] = v[r];
+                }
+            } else {
+                bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pix * a.ldy + n;
+                if (accum) {
+                    if (full) {
+                        const u32x2 o = *reinterpret_cast<const u32x2*>(y);
+                        v[0] += lo_bf(o[0]); v[1] += hi_bf(o[0]); v[2] += lo_bf(o[1]); v[3] += hi_bf(o[1]);
+                    } else {
+                        for (int r = 0; r < 4; ++r)
+                            if (n + r < a.Nout) v[r] += bf2f(y[r]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (relu) v[r] = fmaxf(v[r], 0.f);
+                const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
+                if (full) {
+                    *reinterpret_cast<u32x2*>(y) = u32x2{lo, hi};
+                } else {
+                    const bf16_t h[4] = {(bf16_t)(lo & 0xffff), (bf16_t)(lo >> 16), (bf16_t)(hi & 0xffff),
+                                         (bf16_t)(hi >> 16)};
+                    for (int r = 0; r < 4; ++r)
+                        if (n + r < a.Nout) y[r] = h[r];
+                }
+                // statistics of the values BN will actually read (bf16-rounded)
+                v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
+            }
+            if (st) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    s1[i][r] += v[r];
+                    s2[i][r] += v[r] * v[r];
+                }
+            }
+        }
+    }
+    if (st) {
+        // Every tile adds into the same 2*Nout words: contention, not bytes,
+        // bounds this (MI355X_MICROARCH.md "Global float atomics": one hot row
+        // is ~14x slower). Adds are spread over STAT_SLOTS copies by block id
+        // (neighbouring blocks sit on different XCDs) and issued as one 16-lane
+        // instruction per 16 consecutive channels; imk_bn_stats_finalize folds
+        // the slots.
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            float v1 = 0.f, v2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x1 = s1[i][r], x2 = s2[i][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    x1 += __shfl_xor(x1, o, 64);
+                    x2 += __shfl_xor(x2, o, 64);
+                }
+                if ((lane & 15) == r) {
+                    v1 = x1;
+                    v2 = x2;
+                }
+            }
+            const int n = nb + i * 16 + (lane & 15);
+            if ((lane & 15) < 4 && n < a.Nout) {
+                atomicAdd(st + n, v1);
+                atomicAdd(st + a.Nout + n, v2);
+            }
+        }
+    }
+}
+
+// MFMA over one 64-deep stage held in LDS (rows of 128 B, chunk-swizzled)
+template <int FN, int FM>
+__device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* bx, const bf16_t* bw, int fk0,
+                                           int fk1) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 fw[FN], fx[FM];
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+            fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + (ks ? fk1 : fk0));
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+            fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + (ks ? fk1 : fk0));
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[i], fx[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// ======================================================= LDS-DMA ring kernel
+template <int BM, int BN, int WN, int NS, int MODE>  // MODE 0: C%64==0, 1: C%8==0
+__global__ __launch_bounds__(256, 2) void igemm_dma_kernel(const IGemmArgs a) {
+    constexpr int WM = 4 / WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    constexpr int QA = BM / 32, QB = BN / 32;  // DMA pieces (8 rows each) per wave per stage
+    constexpr int LPS = QA + QB;               // vmcnt units per stage
+    constexpr int SA = BM * LDK, SB = BN * LDK;  // elements per stage buffer
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* sX = reinterpret_cast<bf16_t*>(smem);  // [NS][BM][64]
+    bf16_t* sW = sX + NS * SA;                     // [NS][BN][64]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wid % WN, wm = wid / WN;
+    const int nbn = (a.Nout + BN - 1) / BN;
+    const int nbm = (a.M + BM - 1) / BM;
+    const int ntiles = nbm * nbn;
+    const int G = gridDim.x;
+    const int lid = xcd_remap(blockIdx.x, G);
+    if (lid >= ntiles) return;
+    const int my_tiles = (ntiles - lid + G - 1) / G;
+    const int K = a.nth * a.ntw * a.C;
+    const int nk = max(1, (K + BK - 1) / BK);
+    const int nstages = my_tiles * nk;
+    const int ohw = a.OH * a.OW;
+    // this lane's DMA slot: row (lane>>3) of each 8-row piece, physical chunk
+    // lane&7 -> logical chunk (lane&7) ^ (row & 7)   (row & 7 == lane >> 3)
+    const int lrow = lane >> 3;
+    const int lchunk = (lane & 7) ^ lrow;
+    const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_igemm_zero);
+
+    // gather state of the tile being LOADED (rows wid*QA*8 + q*8 + lrow)
+    const bf16_t* xrow[QA];
+    int ih0[QA], iw0[QA];
+    bool mok[QA];
+    const bf16_t* wrow[QB];
+    bool nok[QB];
+    auto setup_rows = [&](int tile) {
+        const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int m = m0 + (wid * QA + q) * 8 + lrow;
+            mok[q] = m < a.M;
+            const int mm = mok[q] ? m : 0;
+            const int img = mm / ohw, rem = mm - img * ohw;
+            const int oh = rem / a.OW, ow = rem - oh * a.OW;
+            xrow[q] = a.X + (size_t)img * a.H * a.W * a.C;
+            ih0[q] = oh * a.sA;
+            iw0[q] = ow * a.sA;
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int n = n0 + (wid * QB + q) * 8 + lrow;
+            nok[q] = n < a.Nout;
+            wrow[q] = a.Wk + (size_t)(nok[q] ? n : 0) * a.ldb;
+        }
+    };
+    auto issue = [&](int kt, int buf) {
+        int t, c;
+        const int k = kt * BK + lchunk * 8;
+        if (MODE == 0) {
+            t = (kt * BK) / a.C;
+            c = kt * BK - t * a.C + lchunk * 8;
+        } else {
+            t = k / a.C;
+            c = k - t * a.C;
+        }
+        const bool kok = k < K;
+        const int ti = kok ? t / a.ntw : 0, tj = kok ? t - ti * a.ntw : 0;
+        const int dh = a.dh0 + ti * a.dhs, dw = a.dw0 + tj * a.dws;
+        const int wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
+        char* dX = reinterpret_cast<char*>(sX + buf * SA) + (wid * QA) * 1024;
+        char* dW = reinterpret_cast<char*>(sW + buf * SB) + (wid * QB) * 1024;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int ih = ih0[q] + dh, iw = iw0[q] + dw;
+            const bool ok = kok && mok[q] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+            const bf16_t* src = ok ? xrow[q] + ((size_t)ih * a.W + iw) * a.C + c : zero;
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                             (void __attribute__((address_space(3)))*)(dX + q * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const bf16_t* src = (kok && nok[q]) ? wrow[q] + wtap * a.C + c : zero;
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                             (void __attribute__((address_space(3)))*)(dW + q * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout : nullptr;
+
+    // issue cursor (stage index + its tile / kt)
+    int is = 0, itj = 0, ikt = 0;
+    auto issue_next = [&]() {
+        if (is < nstages) {
+            if (ikt == 0) setup_rows(lid + itj * G);
+            issue(ikt, is % NS);
+            ++is;
+            if (++ikt == nk) {
+                ikt = 0;
+                ++itj;
+            }
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue_next();
+
+    const int fr = lane & 15;
+    const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
+    int tj = 0, kt = 0;
+    for (int s = 0; s < nstages; ++s) {
+        // stage s landed for this wave when at most (stages issued after s) x LPS remain
+        // (steady state: NS-2 stages beyond s are in flight; near the end fewer -> drain)
+        if (is - 1 - s >= NS - 2)
+            __builtin_amdgcn_s_waitcnt((((NS - 2) * LPS) & 0xF) | ((((NS - 2) * LPS) >> 4) << 14) | (0x7 << 4) |
+                                       (0xF << 8));
+        else
+            __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (s-1)%NS is free
+        issue_next();
+        const int buf = s % NS;
+        mfma_stage<FN, FM>(acc, sX + buf * SA + (wm * TM + fr) * LDK, sW + buf * SB + (wn * TN + fr) * LDK,
+                           fk0, fk1);
+        if (++kt == nk) {
+            const int tile = lid + tj * G;
+            const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
+            epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            kt = 0;
+            ++tj;
+        }
+    }
+}
+
+// ================================================= register-staged kernel
 template <int BM, int BN, int WN, int MODE>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
-__global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
+__global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
     constexpr int WM = 4 / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 16, FN = TN / 16;
@@ -87,12 +388,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     if (lid >= ntiles) return;
     const int my_tiles = (ntiles - lid + G - 1) / G;
     const int K = MODE == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
-    const int nk = max(1, (K + BK - 1) / BK);  // K == 0 (empty dgrad class): one zero stage
+    const int nk = max(1, (K + BK - 1) / BK);
     const int nstages = my_tiles * nk;
     const int col8 = tid & 7;
     const int ohw = a.OH * a.OW;
 
-    // gather-row state of the tile currently being LOADED
     const bf16_t* xrow[A_CH];
     int ih0[A_CH], iw0[A_CH];
     bool mok[A_CH];
@@ -147,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
         }
         const int k = kt * BK + col8 * 8;
         int t, c;
-        if (MODE == 0) {  // C % 64 == 0: the whole K stage sits in one tap
+        if (MODE == 0) {
             t = (kt * BK) / a.C;
             c = kt * BK - t * a.C + col8 * 8;
         } else {
@@ -189,126 +489,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU, accum = a.flags & IG_ACCUM;
     float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout : nullptr;
 
-    // ---------------- epilogue of one output tile ----------------
-    // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
-    auto epilogue = [&](int tile) {
-        const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-        const int nb = n0 + wn * TN + (lane >> 4) * 4;
-        const int mb = m0 + wm * TM + (lane & 15);
-        float s1[FN][4], s2[FN][4];
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-            const int m = mb + j * 16;
-            if (m >= a.M) continue;
-            const int img = m / ohw, rem = m - img * ohw;
-            const int oh = rem / a.OW, ow = rem - oh * a.OW;
-            const size_t pix = ((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox;
-#pragma unroll
-            for (int i = 0; i < FN; ++i) {
-                const int n = nb + i * 16;
-                if (n >= a.Nout) continue;
-                const bool full = n + 3 < a.Nout && (a.ldy % 4) == 0;
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[r] = acc[i][j][r];
-                    if (a.bias) v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
-                }
-                if (out_f32) {
-                    float* y = reinterpret_cast<float*>(a.Y) + pix * a.ldy + n;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (relu) v[r] = fmaxf(v[r], 0.f);
-                    if (full) {
-                        *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
-                    } else {
-                        for (int r = 0; r < 4; ++r)
-                            if (n + r < a.Nout) y[r] = v[r];
-                    }
-                } else {
-                    bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pix * a.ldy + n;
-                    if (accum) {
-                        if (full) {
-                            const u32x2 o = *reinterpret_cast<const u32x2*>(y);
-                            v[0] += lo_bf(o[0]); v[1] += hi_bf(o[0]); v[2] += lo_bf(o[1]); v[3] += hi_bf(o[1]);
-                        } else {
-                            for (int r = 0; r < 4; ++r)
-                                if (n + r < a.Nout) v[r] += bf2f(y[r]);
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (relu) v[r] = fmaxf(v[r], 0.f);
-                    const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
-                    if (full) {
-                        *reinterpret_cast<u32x2*>(y) = u32x2{lo, hi};
-                    } else {
-                        const bf16_t h[4] = {(bf16_t)(lo & 0xffff), (bf16_t)(lo >> 16), (bf16_t)(hi & 0xffff),
-                                             (bf16_t)(hi >> 16)};
-                        for (int r = 0; r < 4; ++r)
-                            if (n + r < a.Nout) y[r] = h[r];
-                    }
-                    // statistics of the values BN will actually read (bf16-rounded)
-                    v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
-                }
-                if (st) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        s1[i][r] += v[r];
-                        s2[i][r] += v[r] * v[r];
-                    }
-                }
-            }
-        }
-        if (st) {
-            // Every tile adds into the same 2*Nout words: contention, not bytes,
-            // bounds this (MI355X_MICROARCH.md "Global float atomics": one hot
-            // row is ~14x slower). Adds are spread over STAT_SLOTS copies by
-            // block id (neighbouring blocks sit on different XCDs) and issued as
-            // one 16-lane instruction per 16 consecutive channels;
-            // imk_bn_stats_finalize folds the slots.
-#pragma unroll
-            for (int i = 0; i < FN; ++i) {
-                float v1 = 0.f, v2 = 0.f;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float x1 = s1[i][r], x2 = s2[i][r];
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        x1 += __shfl_xor(x1, o, 64);
-                        x2 += __shfl_xor(x2, o, 64);
-                    }
-                    if ((lane & 15) == r) {
-                        v1 = x1;
-                        v2 = x2;
-                    }
-                }
-                const int n = nb + i * 16 + (lane & 15);
-                if ((lane & 15) < 4 && n < a.Nout) {
-                    atomicAdd(st + n, v1);
-                    atomicAdd(st + a.Nout + n, v2);
-                }
-            }
-        }
-    };
-
-    // ---------------- flattened (tile, K-stage) pipeline ----------------
     setup_rows(lid);
     load_stage(0);
     store_stage(0);
     __syncthreads();
     const int fr = lane & 15;
-    // physical chunk of logical chunk (lane>>4) + 4*ks in a row with (row & 7) == (fr & 7)
     const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
-    int tj = 0, kt = 0;  // tile ordinal / stage within tile of stage s
+    int tj = 0, kt = 0;
     for (int s = 0; s < nstages; ++s) {
         const int buf = s & 1;
         const bool has_next = s + 1 < nstages;
@@ -320,25 +509,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
                 load_stage(kt + 1);
             }
         }
-        const bf16_t* bx = sX + buf * BM * LDK + (wm * TM + fr) * LDK;
-        const bf16_t* bw = sW + buf * BN * LDK + (wn * TN + fr) * LDK;
-#pragma unroll
-        for (int ks = 0; ks < BK / 32; ++ks) {
-            bf16x8 fw[FN], fx[FM];
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-                fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + (ks ? fk1 : fk0));
-#pragma unroll
-            for (int j = 0; j < FM; ++j)
-                fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + (ks ? fk1 : fk0));
-#pragma unroll
-            for (int i = 0; i < FN; ++i)
-#pragma unroll
-                for (int j = 0; j < FM; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[i], fx[j], acc[i][j], 0, 0, 0);
-        }
+        mfma_stage<FN, FM>(acc, sX + buf * BM * LDK + (wm * TM + fr) * LDK,
+                           sW + buf * BN * LDK + (wn * TN + fr) * LDK, fk0, fk1);
         if (kt + 1 == nk) {
-            epilogue(lid + tj * G);
+            const int tile = lid + tj * G;
+            const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
+            epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -353,29 +529,46 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     }
 }
 
+template <typename KernelT>
+int resident_blocks(KernelT kern, size_t lds) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    return per_cu * cus;
+}
+
+// persistent only where it pays: tiles with few K-stages (memory-bound 1x1
+// convs) overlap the next tile's loads with this tile's epilogue; long-K tiles
+// keep one tile per block (the hardware refills CUs without a tail)
+inline int grid_size(int ntiles, int nk, int resident) {
+    return (nk > 4 || ntiles < resident) ? ntiles : resident;
+}
+
+template <int BM, int BN, int WN, int NS, int MD>
+int launch_dma(const IGemmArgs& a, hipStream_t st) {
+    const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+    const size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
+    static int resident = 0;
+    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD>, lds);
+    const int nk = (a.nth * a.ntw * a.C + BK - 1) / BK;
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD>), dim3(grid_size(ntiles, nk, resident)), dim3(256),
+                       lds, st, a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
 template <int BM, int BN, int WN, int MD>
-int launch(const IGemmArgs& a, hipStream_t st) {
-    const int nbm = (a.M + BM - 1) / BM, nbn = (a.Nout + BN - 1) / BN;
-    const int ntiles = nbm * nbn;
+int launch_rs(const IGemmArgs& a, hipStream_t st) {
+    const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
-    static int resident = 0;  // persistent grid = blocks resident per CU x CUs (queried once)
-    if (resident == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, igemm_kernel<BM, BN, WN, MD>, 256, lds) !=
-            hipSuccess || per_cu < 1)
-            per_cu = 1;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        resident = per_cu * cus;
-    }
-    // persistent only where it pays: tiles with few K-stages (memory-bound 1x1
-    // convs) overlap the next tile's loads with this tile's epilogue; long-K
-    // tiles keep one tile per block (the hardware refills CUs without a tail)
+    static int resident = 0;
+    if (resident == 0) resident = resident_blocks(igemm_rs_kernel<BM, BN, WN, MD>, lds);
     const int K = MD == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
-    const int nk = (K + BK - 1) / BK;
-    const int grid = (nk > 4 || ntiles < resident) ? ntiles : resident;
-    hipLaunchKernelGGL((igemm_kernel<BM, BN, WN, MD>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD>), dim3(grid_size(ntiles, (K + BK - 1) / BK, resident)),
+                       dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -390,20 +583,31 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if ((a.flags & IG_ACCUM) && (a.flags & IG_OUT_F32)) return -103;
     if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32
         if (a.C != 4 || a.ntw > 8 || a.dhs != 1 || a.dws != 1) return -102;
-        return launch<128, 64, 1, 2>(a, st);
+        return launch_rs<128, 64, 1, 2>(a, st);
     }
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     const int md = (a.C % BK) == 0 ? 0 : 1;
     if (tile == 0) tile = (a.Nout <= 64) ? 4 : 2;
-#define IG_L(BM_, BN_, WN_) (md == 0 ? launch<BM_, BN_, WN_, 0>(a, st) : launch<BM_, BN_, WN_, 1>(a, st))
+    if (a.flags & IG_REGSTAGE) {
+#define IG_RS(BM_, BN_, WN_) (md == 0 ? launch_rs<BM_, BN_, WN_, 0>(a, st) : launch_rs<BM_, BN_, WN_, 1>(a, st))
+        switch (tile) {
+            case 2: return IG_RS(128, 128, 2);
+            case 4: return IG_RS(128, 64, 1);
+            default: return -101;
+        }
+#undef IG_RS
+    }
+#define IG_D(BM_, BN_, WN_, NS_) \
+    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0>(a, st) : launch_dma<BM_, BN_, WN_, NS_, 1>(a, st))
     switch (tile) {
-        case 1: return IG_L(256, 64, 1);
-        case 2: return IG_L(128, 128, 2);
-        case 3: return IG_L(64, 128, 4);
-        case 4: return IG_L(128, 64, 1);
+        case 1: return IG_D(256, 64, 1, 2);
+        case 2: return IG_D(128, 128, 2, 2);
+        case 3: return IG_D(64, 128, 4, 3);
+        case 4: return IG_D(128, 64, 1, 3);
+        case 5: return IG_D(128, 128, 2, 3);
         default: return -101;
     }
-#undef IG_L
+#undef IG_D
 }
 
 IMK_EXPORT int imk_igemm_args_size() { return (int)sizeof(IGemmArgs); }
