@@ -588,7 +588,12 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     const int md = (a.C % BK) == 0 ? 0 : 1;
     if (tile == 0) tile = (a.Nout <= 64) ? 4 : 2;
-    if (a.flags & IG_REGSTAGE) {
+    // measured on MI355X (profiles/r50_conv_layers_*): the register-staged
+    // pipeline wins for 64-wide output tiles and single-stage (K <= 64) tiles,
+    // the LDS-DMA ring for everything with a real K loop
+    const int K = a.nth * a.ntw * a.C;
+    const bool regstage = (a.flags & IG_REGSTAGE) || a.Nout <= 64 || K <= BK;
+    if (regstage) {
 #define IG_RS(BM_, BN_, WN_) (md == 0 ? launch_rs<BM_, BN_, WN_, 0>(a, st) : launch_rs<BM_, BN_, WN_, 1>(a, st))
         switch (tile) {
             case 2: return IG_RS(128, 128, 2);

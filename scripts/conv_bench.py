@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--miopen", action="store_true")
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
+    ap.add_argument("--no-stats", action="store_true", help="forward without the fused BN statistics")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
     dev = "cuda"
@@ -85,7 +86,7 @@ def main():
         wt = w.permute(3, 1, 2, 0).contiguous() if not stem else None
         dy = torch.randn(B, OH, OH, Co, device=dev).to(torch.bfloat16)
         dw = torch.zeros(Co, k, 32, device=dev) if stem else torch.zeros(Co, k, k, Cin, device=dev)
-        stats = torch.zeros(32, 2, Co, device=dev)
+        stats = None if a.no_stats else torch.zeros(32, 2, Co, device=dev)
         flops = 2.0 * B * OH * OH * Co * k * k * Ci
         t_f = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, stem=stem))
         t_d = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k)) if not stem else 0.0
