@@ -95,6 +95,11 @@ __device__ __forceinline__ void waitcnt_vm(int n) {
 }
 
 // ------------------------------------------------------------------ epilogue
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
 template <int FN, int FM>
 __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb,
@@ -174,29 +179,45 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
         // Every tile adds into the same 2*Nout words: contention, not bytes,
         // bounds this (MI355X_MICROARCH.md "Global float atomics": one hot row
         // is ~14x slower). Adds are spread over STAT_SLOTS copies by block id
-        // (neighbouring blocks sit on different XCDs) and issued as one 16-lane
-        // instruction per 16 consecutive channels; imk_bn_stats_finalize folds
-        // the slots.
+        // (neighbouring blocks sit on different XCDs); imk_bn_stats_finalize
+        // folds the slots.
+        //
+        // The 8 partial sums (4 channels x {sum, sumsq}) of a lane are reduced
+        // over the 16 lanes of its DPP row by a transpose-reduce: xor-1 and
+        // xor-2 exchanges each halve the values a lane carries (4 + 2 DPP adds),
+        // then row rotations by 4 and 8 finish the 4-lane groups (2 x 2 adds):
+        // 10 v_add_f32_dpp per fragment instead of 32 ds_bpermute + 32 adds.
+        const int l = lane & 15;
+        const bool b0 = l & 1, b1 = (l >> 1) & 1;
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
-            float v1 = 0.f, v2 = 0.f;
+            float v[8];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float x1 = s1[i][r], x2 = s2[i][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    x1 += __shfl_xor(x1, o, 64);
-                    x2 += __shfl_xor(x2, o, 64);
-                }
-                if ((lane & 15) == r) {
-                    v1 = x1;
-                    v2 = x2;
-                }
+                v[2 * r] = s1[i][r];
+                v[2 * r + 1] = s2[i][r];
             }
-            const int n = nb + i * 16 + (lane & 15);
-            if ((lane & 15) < 4 && n < a.Nout) {
-                atomicAdd(st + n, v1);
-                atomicAdd(st + a.Nout + n, v2);
+            float w[4], u[2];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float keep = b0 ? v[4 + j] : v[j], send = b0 ? v[j] : v[4 + j];
+                w[j] = keep + dpp_f32<0xB1>(send);  // quad_perm [1,0,3,2]
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float keep = b1 ? w[2 + t] : w[t], send = b1 ? w[t] : w[2 + t];
+                u[t] = keep + dpp_f32<0x4E>(send);  // quad_perm [2,3,0,1]
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                u[t] += dpp_f32<0x124>(u[t]);  // row_ror:4
+                u[t] += dpp_f32<0x128>(u[t]);  // row_ror:8
+            }
+            // lane l < 4 holds channel r = 2*b0 + b1: u[0] = sum, u[1] = sumsq
+            const int n = nb + i * 16 + 2 * b0 + b1;
+            if (l < 4 && n < a.Nout) {
+                atomicAdd(st + n, u[0]);
+                atomicAdd(st + a.Nout + n, u[1]);
             }
         }
     }
