@@ -245,12 +245,15 @@ __device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* b
 }
 
 // ======================================================= LDS-DMA ring kernel
-template <int BM, int BN, int WN, int NS, int MODE>  // MODE 0: C%64==0, 1: C%8==0
-__global__ __launch_bounds__(256, 2) void igemm_dma_kernel(const IGemmArgs a) {
-    constexpr int WM = 4 / WN;
+// NW waves per block (4: two blocks per CU; 8: one big-tile block per CU,
+// two waves per SIMD, fewer L2->LDS bytes per MFMA FLOP)
+template <int BM, int BN, int WN, int NS, int MODE, int NW>  // MODE 0: C%64==0, 1: C%8==0
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
+    constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 16, FN = TN / 16;
-    constexpr int QA = BM / 32, QB = BN / 32;  // DMA pieces (8 rows each) per wave per stage
+    constexpr int QA = BM / (8 * NW), QB = BN / (8 * NW);  // DMA pieces (8 rows each) per wave per stage
+    static_assert(QA >= 1 && QB >= 1 && WM * WN == NW, "tile / wave split");
     constexpr int LPS = QA + QB;               // vmcnt units per stage
     constexpr int SA = BM * LDK, SB = BN * LDK;  // elements per stage buffer
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -551,9 +554,9 @@ __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
 }
 
 template <typename KernelT>
-int resident_blocks(KernelT kern, size_t lds) {
+int resident_blocks(KernelT kern, size_t lds, int threads = 256) {
     int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -568,15 +571,15 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     const size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD>, lds);
+    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW>, lds, NW * 64);
     const int nk = (a.nth * a.ntw * a.C + BK - 1) / BK;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD>), dim3(grid_size(ntiles, nk, resident)), dim3(256),
-                       lds, st, a);
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW>), dim3(grid_size(ntiles, nk, resident)),
+                       dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -608,12 +611,22 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     }
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     const int md = (a.C % BK) == 0 ? 0 : 1;
-    if (tile == 0) tile = (a.Nout <= 64) ? 4 : 2;
+    const bool autotile = tile == 0;
+    if (autotile) tile = (a.Nout <= 64) ? 4 : 2;
     // measured on MI355X (profiles/r50_conv_layers_*): the register-staged
     // pipeline wins for 64-wide output tiles and single-stage (K <= 64) tiles,
     // the LDS-DMA ring for everything with a real K loop
     const int K = a.nth * a.ntw * a.C;
-    const bool regstage = (a.flags & IG_REGSTAGE) || a.Nout <= 64 || K <= BK;
+    const bool regstage = (a.flags & IG_REGSTAGE) || (autotile && (a.Nout <= 64 || K <= BK));
+    // 256x256 tiles (8 waves, one block per CU) halve the L2->LDS bytes per
+    // MFMA FLOP -- the measured limiter of the 128x128 tile (~70 GB/s per CU
+    // of gathered rows, profiles/r50_conv_tiles_*.md) -- but only pay when
+    // the output is >= 256 channels wide and there are enough of them to
+    // occupy the chip
+    if (autotile && !regstage && a.Nout >= 256) {
+        const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+        if (t8 >= 192) tile = 8;
+    }
     if (regstage) {
 #define IG_RS(BM_, BN_, WN_) (md == 0 ? launch_rs<BM_, BN_, WN_, 0>(a, st) : launch_rs<BM_, BN_, WN_, 1>(a, st))
         switch (tile) {
@@ -623,14 +636,18 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
 #undef IG_RS
     }
-#define IG_D(BM_, BN_, WN_, NS_) \
-    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0>(a, st) : launch_dma<BM_, BN_, WN_, NS_, 1>(a, st))
+#define IG_D(BM_, BN_, WN_, NS_, NW_) \
+    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_>(a, st) : launch_dma<BM_, BN_, WN_, NS_, 1, NW_>(a, st))
     switch (tile) {
-        case 1: return IG_D(256, 64, 1, 2);
-        case 2: return IG_D(128, 128, 2, 2);
-        case 3: return IG_D(64, 128, 4, 3);
-        case 4: return IG_D(128, 64, 1, 3);
-        case 5: return IG_D(128, 128, 2, 3);
+        case 1: return IG_D(256, 64, 1, 2, 4);
+        case 2: return IG_D(128, 128, 2, 2, 4);
+        case 3: return IG_D(64, 128, 4, 3, 4);
+        case 4: return IG_D(128, 64, 1, 3, 4);
+        case 5: return IG_D(128, 128, 2, 3, 4);
+        case 6: return IG_D(256, 128, 2, 3, 8);  // 144 KiB LDS, 8 waves of 64x64
+        case 7: return IG_D(128, 256, 4, 3, 8);
+        case 8: return IG_D(256, 256, 2, 2, 8);  // 128 KiB LDS, 8 waves of 64x128
+        case 9: return IG_D(256, 128, 2, 2, 8);
         default: return -101;
     }
 #undef IG_D

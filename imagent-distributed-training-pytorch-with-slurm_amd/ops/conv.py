@@ -78,7 +78,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
 
 def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
                 KH: int, KW: int, out: Optional[torch.Tensor] = None,
-                accumulate: bool = False) -> torch.Tensor:
+                accumulate: bool = False, tile: int = 0) -> torch.Tensor:
     """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci,KH,KW,Co]).
 
     Stride 1: one gather-GEMM launch with the taps mirrored.
@@ -116,7 +116,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
             a.flags = 8 if accumulate else 0
-            _lib.check(k.imk_conv_igemm(C.byref(a), 0, st), "conv dgrad")
+            _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")
     return out
 
 

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
     ap.add_argument("--no-stats", action="store_true", help="forward without the fused BN statistics")
+    ap.add_argument("--tiles", default=None, help="comma list of explicit tile ids to time for fwd/dgrad")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
     dev = "cuda"
@@ -103,6 +104,13 @@ def main():
             t_m = timeit(lambda: F.conv2d(xc, wc, None, s, p))
             line += f" | {t_m:8.1f}"
             r["miopen_fwd_us"] = t_m
+        if a.tiles and not stem:
+            for t in (int(v) for v in a.tiles.split(",")):
+                tf = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, tile=t))
+                td = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, tile=t))
+                line += f"\n      tile {t}: fwd {tf:8.1f} us {flops / tf / 1e6:6.0f} TF | dgrad {td:8.1f} us " \
+                        f"{flops / td / 1e6:6.0f} TF"
+                r[f"tile{t}"] = (tf, td)
         print(line, flush=True)
         rows.append(r)
         tot["fwd"] += t_f * cnt

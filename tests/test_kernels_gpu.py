@@ -77,6 +77,28 @@ def test_conv_fwd_dgrad_wgrad(shape):
     assert rel(dw.permute(0, 3, 1, 2), 2 * wr.grad) < 5e-3
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 320, 1, 1, 0)])
+def test_conv_explicit_tiles(tile, shape):
+    """Every main-loop / tile variant the dispatcher can pick, incl. ragged tails."""
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(1)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = bf(torch.randn(Co, Ci, k, k, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5)
+    xr = x.float().requires_grad_(True)
+    yr = F.conv2d(xr, w.float(), None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(nhwc(x), nhwc(w), s, p, k, k, stats=slab, tile=tile)
+    assert rel(nchw(y), yr) < 1e-2
+    yb = nchw(y).float()
+    assert rel(slab.sum(0)[0], yb.sum((0, 2, 3))) < 1e-3
+    dx = igemm_dgrad(nhwc(g), w.permute(1, 2, 3, 0).contiguous(), (H, H), s, p, k, k, tile=tile)
+    assert rel(nchw(dx), xr.grad) < 1e-2
+
+
 def test_stem_row_segment_conv():
     """7x7/s2 stem: 4-channel NHWC input, [Co][KH][32] weight rows (fwd + wgrad)."""
     from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
