@@ -26,6 +26,9 @@
 
 namespace {
 
+constexpr int U = 4;  // rows per thread per loop iteration (loads batched ahead of the math)
+constexpr int BWD_SLOTS = 32;  // backward reduction slab slots
+
 struct Vec8 {
     float v[8];
 };
@@ -101,25 +104,32 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
             }
         }
     }
-    for (long r = (long)blockIdx.x * rpb + tid / cpr; r < R; r += (long)gridDim.x * rpb) {
-        const size_t off = (size_t)r * C + c0;
-        Vec8 v = ld8(x + off);
+    // U rows per thread per iteration, all loads issued before any math: 4x
+    // the bytes in flight of a one-row loop (HBM needs ~72 KiB per CU)
+    const long step = (long)gridDim.x * rpb;
+    for (long r0 = (long)blockIdx.x * rpb + tid / cpr; r0 < R; r0 += U * step) {
+        Vec8 v[U], s[U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v.v[i] = fmaf(v.v[i], sc[i], sh[i]);
-        if (MODE == 1) {
-            const Vec8 s = ld8(x2 + off);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v.v[i] += s.v[i];
-        } else if (MODE == 2) {
-            const Vec8 s = ld8(x2 + off);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v.v[i] += fmaf(s.v[i], sc2[i], sh2[i]);
+        for (int u = 0; u < U; ++u) {
+            const long r = r0 + u * step;
+            if (r < R) {
+                v[u] = ld8(x + (size_t)r * C + c0);
+                if (MODE != 0) s[u] = ld8(x2 + (size_t)r * C + c0);
+            }
         }
-        if (RELU) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v.v[i] = fmaxf(v.v[i], 0.f);
+        for (int u = 0; u < U; ++u) {
+            const long r = r0 + u * step;
+            if (r >= R) break;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                float o = fmaf(v[u].v[i], sc[i], sh[i]);
+                if (MODE == 1) o += s[u].v[i];
+                if (MODE == 2) o += fmaf(s[u].v[i], sc2[i], sh2[i]);
+                v[u].v[i] = RELU ? fmaxf(o, 0.f) : o;
+            }
+            st8(y + (size_t)r * C + c0, v[u]);
         }
-        st8(y + off, v);
     }
 }
 
@@ -147,12 +157,12 @@ __global__ void bn_running_kernel(const RunDesc* __restrict__ d, int n) {
 
 // Fold the conv epilogue's [S][2][C] statistics slab into [2][C] sums.
 __global__ __launch_bounds__(64) void stats_finalize_kernel(const float* __restrict__ slab,
-                                                            float* __restrict__ out, int S, int n2c) {
+                                                            float* __restrict__ out, int S, int n) {
     const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= n2c) return;
+    if (i >= n) return;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-    for (int k = 0; k < S; ++k) s[k & 3] += slab[(size_t)k * n2c + i];
+    for (int k = 0; k < S; ++k) s[k & 3] += slab[(size_t)k * n + i];
     out[i] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
@@ -160,10 +170,9 @@ __global__ __launch_bounds__(64) void stats_finalize_kernel(const float* __restr
 // MASK 0: no ReLU; 1: ReLU mask from the saved output y; 2: from x (mode 0 only:
 // y = relu(fma(x, sc, sh)) with the forward's sc = rstd*gamma, sh = beta - mean*sc)
 template <int MASK>
-__device__ __forceinline__ void relu_mask(Vec8& g, const bf16_t* y, const Vec8& xv, const float* sc,
+__device__ __forceinline__ void relu_mask(Vec8& g, const u32x4& yw, const Vec8& xv, const float* sc,
                                           const float* sh) {
     if (MASK == 1) {
-        const u32x4 yw = *reinterpret_cast<const u32x4*>(y);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (!(lo_bf(yw[i]) > 0.f)) g.v[2 * i] = 0.f;
@@ -206,20 +215,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         acc[0][i] = acc[1][i] = acc[2][i] = 0.f;
     }
     if (active) {
-        for (long r = (long)blockIdx.x * rpb + rsub; r < R; r += (long)gridDim.x * rpb) {
-            const size_t off = (size_t)r * C + c0;
-            Vec8 g = ld8(dy + off);
-            const Vec8 xv = ld8(x + off);
-            relu_mask<MASK>(g, y + off, xv, sc, sh);
+        const long step = (long)gridDim.x * rpb;
+        for (long r0 = (long)blockIdx.x * rpb + rsub; r0 < R; r0 += U * step) {
+            Vec8 g[U], xv[U], x2v[U];
+            u32x4 yv[U];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                acc[0][i] += g.v[i] * (xv.v[i] - mean[i]) * rstd[i];
-                acc[1][i] += g.v[i];
+            for (int u = 0; u < U; ++u) {
+                const long r = r0 + u * step;
+                if (r < R) {
+                    const size_t off = (size_t)r * C + c0;
+                    g[u] = ld8(dy + off);
+                    xv[u] = ld8(x + off);
+                    if (MODE == 2) x2v[u] = ld8(x2 + off);
+                    if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) g[u].v[i] = xv[u].v[i] = x2v[u].v[i] = 0.f;
+                }
             }
-            if (MODE == 2) {
-                const Vec8 x2v = ld8(x2 + off);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) acc[2][i] += g.v[i] * (x2v.v[i] - m2[i]) * r2[i];
+            for (int u = 0; u < U; ++u) {
+                const long r = r0 + u * step;
+                if (r < R) relu_mask<MASK>(g[u], yv[u], xv[u], sc, sh);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    acc[0][i] += g[u].v[i] * (xv[u].v[i] - mean[i]) * rstd[i];
+                    acc[1][i] += g[u].v[i];
+                    if (MODE == 2) acc[2][i] += g[u].v[i] * (x2v[u].v[i] - m2[i]) * r2[i];
+                }
             }
         }
     }
@@ -233,10 +256,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
             for (int i = 0; i < 8; ++i) red[rsub * C + c0 + i] = acc[qi][i];
         }
         __syncthreads();
+        // one add per channel per block into slot (block & 31) of the [32][3][C]
+        // slab: 1024 blocks adding into the same 3*C words serialise at the
+        // memory-side atomic unit (the conv-epilogue statistics lesson)
+        float* slot = scratch + (size_t)(blockIdx.x & (BWD_SLOTS - 1)) * 3 * C;
         for (int c = tid; c < C; c += 256) {
             float s = 0.f;
             for (int rr = 0; rr < rpb; ++rr) s += red[rr * C + c];
-            atomicAdd(scratch + qi * C + c, s);
+            atomicAdd(slot + qi * C + c, s);
         }
     }
 }
@@ -288,30 +315,47 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             q3[i] = -g2 * inv_cnt * scratch[2 * C + c] * rs2;
         }
     }
-    for (long r = (long)blockIdx.x * rpb + tid / cpr; r < R; r += (long)gridDim.x * rpb) {
-        const size_t off = (size_t)r * C + c0;
-        Vec8 g = ld8(dy + off);
-        const Vec8 xv = ld8(x + off);
-        relu_mask<MASK>(g, y + off, xv, sc, sh);
-        Vec8 o;
+    const long step = (long)gridDim.x * rpb;
+    for (long r0 = (long)blockIdx.x * rpb + tid / cpr; r0 < R; r0 += U * step) {
+        Vec8 g[U], xv[U], x2v[U];
+        u32x4 yv[U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g.v[i] + k2[i] + k3[i] * (xv.v[i] - mean[i]);
-        st8(dx + off, o);
-        if (MODE == 1) st8(dres + off, g);
-        if (MODE == 2) {
-            const Vec8 x2v = ld8(x2 + off);
+        for (int u = 0; u < U; ++u) {
+            const long r = r0 + u * step;
+            if (r < R) {
+                const size_t off = (size_t)r * C + c0;
+                g[u] = ld8(dy + off);
+                xv[u] = ld8(x + off);
+                if (MODE == 2) x2v[u] = ld8(x2 + off);
+                if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
+            }
+        }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o.v[i] = q1[i] * g.v[i] + q2[i] + q3[i] * (x2v.v[i] - m2[i]);
-            st8(dx2 + off, o);
+        for (int u = 0; u < U; ++u) {
+            const long r = r0 + u * step;
+            if (r >= R) break;
+            const size_t off = (size_t)r * C + c0;
+            relu_mask<MASK>(g[u], yv[u], xv[u], sc, sh);
+            Vec8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g[u].v[i] + k2[i] + k3[i] * (xv[u].v[i] - mean[i]);
+            st8(dx + off, o);
+            if (MODE == 1) st8(dres + off, g[u]);
+            if (MODE == 2) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    o.v[i] = q1[i] * g[u].v[i] + q2[i] + q3[i] * (x2v[u].v[i] - m2[i]);
+                st8(dx2 + off, o);
+            }
         }
     }
 }
 
 int grid_for(long R, int C) {
     const int rpb = 256 / (C / 8);
-    long blocks = (R + rpb - 1) / rpb;
-    // >= 8 blocks per CU for streaming, then grid-stride (Guideline 11)
-    return (int)(blocks < 4096 ? blocks : 4096);
+    long blocks = (R + U * rpb - 1) / (U * rpb);
+    // 8 resident blocks per CU (2048 threads) for streaming, then grid-stride
+    return (int)(blocks < 2048 ? blocks : 2048);
 }
 
 }  // namespace
@@ -347,6 +391,35 @@ IMK_EXPORT int imk_bn_running_update(const void* descs, int n, void* stream) {
 
 IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
 
+// Apply-only backward for a gradient g that the producing dgrad already
+// ReLU-masked, with its reductions already in the [BWD_SLOTS][3][C] slab of
+// `scratch` (conv epilogue IG_BNBWD): fold + dx (mode 0/1; for mode 1 the
+// caller uses g itself as the residual-branch gradient) or dx, dx2 (mode 2).
+IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save, const float* gamma,
+                                const void* x2, const float* save2, const float* gamma2, float* scratch,
+                                void* dx, void* dx2, float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
+                                float* dbeta2_acc, long R, int C, int mode, void* stream) {
+    if (C % 8 || C > 2048) return -100;
+    hipStream_t st = (hipStream_t)stream;
+    float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
+                       BWD_SLOTS, 3 * C);
+    IMK_CHECK_LAUNCH();
+    const int grid = grid_for(R, C);
+    const float inv_cnt = 1.f / (float)R;
+#define LA(M)                                                                                       \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)g,   \
+                       nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr, \
+                       (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,         \
+                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
+    if (mode == 2) LA(2); else LA(0);
+#undef LA
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 3) * C; }
+
 IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C, void* stream) {
     const int n2c = 2 * C;
     hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2c + 63) / 64), dim3(64), 0, (hipStream_t)stream,
@@ -355,7 +428,8 @@ IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C
     return 0;
 }
 
-// scratch: fp32 [3][C], zero-initialised by the caller.
+// scratch: fp32 [BWD_SLOTS][3][C] slab followed by the folded [3][C], all
+// zero-initialised by the caller.
 // mode 0: plain, 1: also dres (= masked dy, identity residual), 2: also dx2 (downsample BN branch)
 // relu: 0 none, 1 mask from y, 2 mask from x (mode 0 only; needs gamma/beta/save as in forward)
 IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const float* save,
@@ -376,10 +450,14 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     else { if (relu == 2) LR(2, 0); else if (relu) LR(1, 0); else LR(0, 0); }
 #undef LR
     IMK_CHECK_LAUNCH();
+    float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
+                       BWD_SLOTS, 3 * C);
+    IMK_CHECK_LAUNCH();
     const float inv_cnt = 1.f / (float)R;
 #define LA(MK, M)                                                                                  \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
-                       (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, scratch, (bf16_t*)dx,  \
+                       (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, folded, (bf16_t*)dx,   \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
                        dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
     if (mode == 0) { if (relu == 2) LA(2, 0); else if (relu) LA(1, 0); else LA(0, 0); }

@@ -62,6 +62,15 @@ struct IGemmArgs {
     int nth, ntw, dh0, dhs, dw0, dws, kh0, khs, kw0, kws, KW;
     int YH, YW, sY, oy, ox, ldy;
     int flags;         // IG_* bits
+    // IG_BNBWD: the BatchNorm this gradient flows into (all NHWC at the output
+    // pixels, channel stride ldy == Nout)
+    const bf16_t* bnx;     // BN input x
+    const bf16_t* bny;     // BN(+add)+ReLU output for the mask, or null: mask from x
+    const float* bnsave;   // [2][Nout] mean, rstd
+    const float* bngamma;  // used with the from-x mask
+    const float* bnbeta;
+    const bf16_t* bnx2;    // second BN branch input (downsample), or null
+    const float* bnsave2;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
@@ -69,6 +78,7 @@ struct IGemmArgs {
 #define IG_STEM 4      // stem row-segment gather
 #define IG_ACCUM 8     // out += result (bf16 out only): fused gradient accumulation
 #define IG_REGSTAGE 16 // force the register-staged main loop (A/B testing)
+#define IG_BNBWD 32    // epilogue = ReLU mask + BatchNorm-backward reductions (slab [32][3][Nout])
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes
@@ -98,6 +108,56 @@ __device__ __forceinline__ void waitcnt_vm(int n) {
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+// Per-channel partial sums of a fragment -> the stats slab.
+// Every tile adds into the same few Nout-long rows: contention, not bytes,
+// bounds this (MI355X_MICROARCH.md "Global float atomics": one hot row is
+// ~14x slower). Adds are spread over STAT_SLOTS copies by block id
+// (neighbouring blocks sit on different XCDs); a fold kernel sums the slots.
+// The 8 partial sums (4 channels x {A, B}) of a lane are reduced over the 16
+// lanes of its DPP row by a transpose-reduce: xor-1 and xor-2 exchanges each
+// halve the values a lane carries (4 + 2 DPP adds), then row rotations by 4
+// and 8 finish the 4-lane groups (2 x 2 adds): 10 v_add_f32_dpp per fragment
+// instead of 32 ds_bpermute + 32 adds. nb4 = first channel of the lane's
+// 4-channel group; dB may be null.
+__device__ __forceinline__ void stat_pair_atomic(const float (&sa)[4], const float (&sb)[4], float* dA, float* dB,
+                                                 int nb4, int Nout, int lane) {
+    const int l = lane & 15;
+    const bool b0 = l & 1, b1 = (l >> 1) & 1;
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[2 * r] = sa[r];
+        v[2 * r + 1] = sb[r];
+    }
+    float w[4], u[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float keep = b0 ? v[4 + j] : v[j], send = b0 ? v[j] : v[4 + j];
+        w[j] = keep + dpp_f32<0xB1>(send);  // quad_perm [1,0,3,2]
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const float keep = b1 ? w[2 + t] : w[t], send = b1 ? w[t] : w[2 + t];
+        u[t] = keep + dpp_f32<0x4E>(send);  // quad_perm [2,3,0,1]
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        u[t] += dpp_f32<0x124>(u[t]);  // row_ror:4
+        u[t] += dpp_f32<0x128>(u[t]);  // row_ror:8
+    }
+    // lane l < 4 holds channel r = 2*b0 + b1: u[0] = A, u[1] = B
+    const int n = nb4 + 2 * b0 + b1;
+    if (l < 4 && n < Nout) {
+        atomicAdd(dA + n, u[0]);
+        if (dB) atomicAdd(dB + n, u[1]);
+    }
+}
+
+__device__ __forceinline__ void ld4bf(const bf16_t* p, float (&v)[4]) {
+    const u32x2 w = *reinterpret_cast<const u32x2*>(p);
+    v[0] = lo_bf(w[0]); v[1] = hi_bf(w[0]); v[2] = lo_bf(w[1]); v[3] = hi_bf(w[1]);
 }
 
 // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
@@ -176,51 +236,110 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
         }
     }
     if (st) {
-        // Every tile adds into the same 2*Nout words: contention, not bytes,
-        // bounds this (MI355X_MICROARCH.md "Global float atomics": one hot row
-        // is ~14x slower). Adds are spread over STAT_SLOTS copies by block id
-        // (neighbouring blocks sit on different XCDs); imk_bn_stats_finalize
-        // folds the slots.
-        //
-        // The 8 partial sums (4 channels x {sum, sumsq}) of a lane are reduced
-        // over the 16 lanes of its DPP row by a transpose-reduce: xor-1 and
-        // xor-2 exchanges each halve the values a lane carries (4 + 2 DPP adds),
-        // then row rotations by 4 and 8 finish the 4-lane groups (2 x 2 adds):
-        // 10 v_add_f32_dpp per fragment instead of 32 ds_bpermute + 32 adds.
-        const int l = lane & 15;
-        const bool b0 = l & 1, b1 = (l >> 1) & 1;
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            float v[8];
+        for (int i = 0; i < FN; ++i) stat_pair_atomic(s1[i], s2[i], st, st + a.Nout, nb + i * 16, a.Nout, lane);
+    }
+}
+
+// IG_BNBWD epilogue (dgrad whose output is the upstream gradient g of a
+// BatchNorm(+add)+ReLU), bf16 output with ldy == Nout, Nout % 8 == 0: the
+// stored value is the ReLU-masked g (mask from the saved output y, or
+// recomputed from the BN input x as fma(x, sc, sh) > 0) and the slab
+// receives sum(g*xhat), sum(g) [, sum(g*xhat2)] (bn.hip row order), so the
+// separate reduce pass over (g, x, y) disappears.
+// Channel-fragment outer, pixel inner: every global read a fragment needs (x,
+// y | x2, the old output when accumulating, BN parameters) is issued for all
+// FM pixels before any is used -- one memory latency per fragment instead of
+// FM -- and only 12 partial sums are live.
+template <int FN, int FM>
+__device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb,
+                                             int lane, float* st) {
+    const bool accum = a.flags & IG_ACCUM;
+    const bool has_y = a.bny != nullptr, has_x2 = a.bnx2 != nullptr;
+    const int ohw = a.OH * a.OW;
+    long pixo[FM];
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const int m = mb + j * 16;
+        const int img = m / ohw, rem = m - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        pixo[j] = m < a.M ? (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const int n = nb + i * 16;
+        if (n >= a.Nout) continue;  // Nout % 8 == 0: a 4-channel group is all in or all out
+        f32x4 mean = *reinterpret_cast<const f32x4*>(a.bnsave + n);
+        f32x4 rstd = *reinterpret_cast<const f32x4*>(a.bnsave + a.Nout + n);
+        f32x4 gam = {0.f, 0.f, 0.f, 0.f}, bet = {0.f, 0.f, 0.f, 0.f}, m2 = gam, r2 = gam;
+        if (!has_y) {
+            gam = *reinterpret_cast<const f32x4*>(a.bngamma + n);
+            bet = *reinterpret_cast<const f32x4*>(a.bnbeta + n);
+        }
+        if (has_x2) {
+            m2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + n);
+            r2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + a.Nout + n);
+        }
+        u32x2 xw[FM], yw[FM], x2w[FM], ow[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            xw[j] = yw[j] = x2w[j] = ow[j] = u32x2{0u, 0u};
+            if (pixo[j] < 0) continue;
+            const size_t e = (size_t)pixo[j] + n;
+            xw[j] = *reinterpret_cast<const u32x2*>(a.bnx + e);
+            if (has_y) yw[j] = *reinterpret_cast<const u32x2*>(a.bny + e);
+            if (has_x2) x2w[j] = *reinterpret_cast<const u32x2*>(a.bnx2 + e);
+            if (accum) ow[j] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(a.Y) + e);
+        }
+        float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            if (pixo[j] < 0) continue;
+            const float xv[4] = {lo_bf(xw[j][0]), hi_bf(xw[j][0]), lo_bf(xw[j][1]), hi_bf(xw[j][1])};
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+            if (accum) {
+                v[0] += lo_bf(ow[j][0]); v[1] += hi_bf(ow[j][0]); v[2] += lo_bf(ow[j][1]); v[3] += hi_bf(ow[j][1]);
+            }
+            if (has_y) {
+                const float yv[4] = {lo_bf(yw[j][0]), hi_bf(yw[j][0]), lo_bf(yw[j][1]), hi_bf(yw[j][1])};
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (!(yv[r] > 0.f)) v[r] = 0.f;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float sc = gam[r] * rstd[r], sh = bet[r] - mean[r] * sc;
+                    if (!(fmaf(xv[r], sc, sh) > 0.f)) v[r] = 0.f;
+                }
+            }
+            const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
+            *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.Y) + (size_t)pixo[j] + n) = u32x2{lo, hi};
+            v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                v[2 * r] = s1[i][r];
-                v[2 * r + 1] = s2[i][r];
+                s1[r] += v[r];
+                s2[r] += v[r] * ((xv[r] - mean[r]) * rstd[r]);
             }
-            float w[4], u[2];
+            if (has_x2) {
+                const float x2v[4] = {lo_bf(x2w[j][0]), hi_bf(x2w[j][0]), lo_bf(x2w[j][1]), hi_bf(x2w[j][1])};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float keep = b0 ? v[4 + j] : v[j], send = b0 ? v[j] : v[4 + j];
-                w[j] = keep + dpp_f32<0xB1>(send);  // quad_perm [1,0,3,2]
-            }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const float keep = b1 ? w[2 + t] : w[t], send = b1 ? w[t] : w[2 + t];
-                u[t] = keep + dpp_f32<0x4E>(send);  // quad_perm [2,3,0,1]
-            }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                u[t] += dpp_f32<0x124>(u[t]);  // row_ror:4
-                u[t] += dpp_f32<0x128>(u[t]);  // row_ror:8
-            }
-            // lane l < 4 holds channel r = 2*b0 + b1: u[0] = sum, u[1] = sumsq
-            const int n = nb + i * 16 + 2 * b0 + b1;
-            if (l < 4 && n < a.Nout) {
-                atomicAdd(st + n, u[0]);
-                atomicAdd(st + a.Nout + n, u[1]);
+                for (int r = 0; r < 4; ++r) s3[r] += v[r] * ((x2v[r] - m2[r]) * r2[r]);
             }
         }
+        stat_pair_atomic(s2, s1, st, st + a.Nout, n, a.Nout, lane);
+        if (has_x2) stat_pair_atomic(s3, s3, st + 2 * a.Nout, nullptr, n, a.Nout, lane);
     }
+}
+
+template <int FN, int FM, bool BNB>
+__device__ __forceinline__ void epilogue(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb, int lane,
+                                         float* st) {
+    if (BNB)
+        epilogue_bnb<FN, FM>(a, acc, nb, mb, lane, st);
+    else
+        epilogue_tile<FN, FM>(a, acc, nb, mb, lane, st);
 }
 
 // MFMA over one 64-deep stage held in LDS (rows of 128 B, chunk-swizzled)
@@ -247,7 +366,7 @@ __device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* b
 // ======================================================= LDS-DMA ring kernel
 // NW waves per block (4: two blocks per CU; 8: one big-tile block per CU,
 // two waves per SIMD, fewer L2->LDS bytes per MFMA FLOP)
-template <int BM, int BN, int WN, int NS, int MODE, int NW>  // MODE 0: C%64==0, 1: C%8==0
+template <int BM, int BN, int WN, int NS, int MODE, int NW, bool BNB>  // MODE 0: C%64==0, 1: C%8==0
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -343,7 +462,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout : nullptr;
+    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * ((a.flags & IG_BNBWD) ? 3 : 2) * a.Nout
+                        : nullptr;
 
     // issue cursor (stage index + its tile / kt)
     int is = 0, itj = 0, ikt = 0;
@@ -380,7 +500,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         if (++kt == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-            epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
+            epilogue<FN, FM, BNB>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -392,7 +512,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
 }
 
 // ================================================= register-staged kernel
-template <int BM, int BN, int WN, int MODE>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
+template <int BM, int BN, int WN, int MODE, bool BNB>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
 __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
     constexpr int WM = 4 / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -513,7 +633,8 @@ __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
     for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout : nullptr;
+    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * ((a.flags & IG_BNBWD) ? 3 : 2) * a.Nout
+                        : nullptr;
 
     setup_rows(lid);
     load_stage(0);
@@ -538,7 +659,7 @@ __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
         if (kt + 1 == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-            epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
+            epilogue<FN, FM, BNB>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -571,27 +692,27 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, bool BNB = false>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     const size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW>, lds, NW * 64);
+    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, BNB>, lds, NW * 64);
     const int nk = (a.nth * a.ntw * a.C + BK - 1) / BK;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW>), dim3(grid_size(ntiles, nk, resident)),
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, BNB>), dim3(grid_size(ntiles, nk, resident)),
                        dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
-template <int BM, int BN, int WN, int MD>
+template <int BM, int BN, int WN, int MD, bool BNB = false>
 int launch_rs(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_rs_kernel<BM, BN, WN, MD>, lds);
+    if (resident == 0) resident = resident_blocks(igemm_rs_kernel<BM, BN, WN, MD, BNB>, lds);
     const int K = MD == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
-    hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD>), dim3(grid_size(ntiles, (K + BK - 1) / BK, resident)),
+    hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD, BNB>), dim3(grid_size(ntiles, (K + BK - 1) / BK, resident)),
                        dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
@@ -605,6 +726,10 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (a.M <= 0 || a.Nout <= 0) return 0;
     if ((a.flags & IG_ACCUM) && (a.flags & IG_OUT_F32)) return -103;
+    if ((a.flags & IG_BNBWD) && ((a.flags & (IG_OUT_F32 | IG_RELU)) || a.Nout % 8 || a.ldy != a.Nout || !a.bnx ||
+                                 !a.bnsave || !a.stats || (!a.bny && (!a.bngamma || !a.bnbeta)) ||
+                                 (a.bnx2 && !a.bnsave2)))
+        return -104;
     if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32
         if (a.C != 4 || a.ntw > 8 || a.dhs != 1 || a.dws != 1) return -102;
         return launch_rs<128, 64, 1, 2>(a, st);
@@ -626,6 +751,21 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (autotile && !regstage && a.Nout >= 256) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
         if (t8 >= 192) tile = 8;
+    }
+    const bool bnb = a.flags & IG_BNBWD;
+    if (bnb) {  // backward-data convs only: the tiles the auto choice makes, fused epilogue
+        if (regstage || (tile != 2 && tile != 8)) {
+            if (tile != 2) tile = 4;
+#define IG_RSB(BM_, BN_, WN_) \
+    (md == 0 ? launch_rs<BM_, BN_, WN_, 0, true>(a, st) : launch_rs<BM_, BN_, WN_, 1, true>(a, st))
+            return tile == 2 ? IG_RSB(128, 128, 2) : IG_RSB(128, 64, 1);
+#undef IG_RSB
+        }
+#define IG_DB(BM_, BN_, WN_, NS_, NW_)                                                  \
+    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, true>(a, st)                       \
+             : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, true>(a, st))
+        return tile == 8 ? IG_DB(256, 256, 2, 2, 8) : IG_DB(128, 128, 2, 2, 4);
+#undef IG_DB
     }
     if (regstage) {
 #define IG_RS(BM_, BN_, WN_) (md == 0 ? launch_rs<BM_, BN_, WN_, 0>(a, st) : launch_rs<BM_, BN_, WN_, 1>(a, st))

@@ -44,14 +44,18 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
     return (uint32_t)(((uint64_t)__umulhi(n, mg) + n) >> sh);
 }
 
-template <int BCO, int BKC, int WCO, bool STEM>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
-    constexpr int WKC = 4 / WCO;
+// NW waves per block: 4 (two blocks per CU) or 8 (one 256x256 block per CU:
+// half the operand bytes per MFMA FLOP of a 128x128 tile)
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void wgrad_kernel(const WgradArgs a) {
+    constexpr int NT = NW * 64;
+    constexpr int WKC = NW / WCO;
     constexpr int TCO = BCO / WCO, TKC = BKC / WKC;
     constexpr int FN = TCO / 16, FM = TKC / 16;
     constexpr int PCO = BCO * 2 + 32, PKC = BKC * 2 + 32;   // LDS row pitch, bytes
     constexpr int CPR_D = BCO / 8, CPR_X = BKC / 8;         // 16-B chunks per row
-    constexpr int D_CH = BR * CPR_D / 256, X_CH = BR * CPR_X / 256;
+    constexpr int D_CH = BR * CPR_D / NT, X_CH = BR * CPR_X / NT;
+    static_assert(D_CH >= 1 && X_CH >= 1 && NT % CPR_D == 0 && NT % CPR_X == 0, "staging split");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sD = smem;                      // [2][BR][PCO]
     char* sX = smem + 2 * BR * PCO;       // [2][BR][PKC]
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         const int mb = mbeg + st * BR;
 #pragma unroll
         for (int i = 0; i < D_CH; ++i) {
-            const int row = (tid + 256 * i) / CPR_D;
+            const int row = (tid + NT * i) / CPR_D;
             const int m = mb + row;
             u32x4 v = {0, 0, 0, 0};
             if (m < mend && dco_ok) v = *reinterpret_cast<const u32x4*>(a.dY + (size_t)m * a.Co + dco);
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < X_CH; ++i) {
-            const int row = (tid + 256 * i) / CPR_X;
+            const int row = (tid + NT * i) / CPR_X;
             const int m = mb + row;
             u32x4 v = {0, 0, 0, 0};
             if (m < mend && xk_ok) {
@@ -136,12 +140,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         char* x = sX + buf * BR * PKC;
 #pragma unroll
         for (int i = 0; i < D_CH; ++i) {
-            const int id = tid + 256 * i;
+            const int id = tid + NT * i;
             *reinterpret_cast<u32x4*>(d + (id / CPR_D) * PCO + (id % CPR_D) * 16) = rd[i];
         }
 #pragma unroll
         for (int i = 0; i < X_CH; ++i) {
-            const int id = tid + 256 * i;
+            const int id = tid + NT * i;
             *reinterpret_cast<u32x4*>(x + (id / CPR_X) * PKC + (id % CPR_X) * 16) = rx[i];
         }
     };
@@ -216,13 +220,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         }
 }
 
-template <int BCO, int BKC, int WCO, bool STEM>
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4>
 int launch(WgradArgs a, int splits, hipStream_t st) {
     const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
     if (splits <= 0) {
-        // ~3 blocks per CU over 256 CUs, at least 4 stages per block
-        const int want = (768 + ntiles - 1) / ntiles;
+        // ~3 blocks per CU over 256 CUs (4-wave blocks, 2 resident per CU) or
+        // ~2 (8-wave blocks, 1 resident), at least 4 stages per block
+        const int target = NW == 4 ? 768 : 512;
+        const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));
     }
@@ -231,7 +237,7 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
-    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM>), dim3(ntiles * splits), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW>), dim3(ntiles * splits), dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -248,6 +254,8 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     }
     if (a.Ci % 8 || a.Co % 8) return -100;
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
+    // (launch<256, 256, 2, false, 8> -- one 8-wave block per CU -- measured 23 %
+    // slower in total: this register-staged loop needs two blocks per CU)
     return launch<128, 128, 2, false>(a, splits, st);
 }
 

@@ -31,7 +31,8 @@ def stem_view(t: torch.Tensor, kw: int) -> torch.Tensor:
 
 
 class NativeState:
-    def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None):
+    def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None,
+                 bnb_fusion: bool = False):
         self.device = torch.device(device)
         named = list(model.named_parameters())
         self.arena = ParamArena(named, self.device, order=order, with_shadow=True)
@@ -39,6 +40,16 @@ class NativeState:
         # one autograd node per residual block with a hand-scheduled backward
         # (ops/block.py); False = per-op autograd nodes (used to cross-check)
         self.fused_blocks = True
+        # BN-backward reductions folded into the producing dgrad epilogue
+        # (ops/block.py). Off by default until the epilogue's extra reads are
+        # coalesced: measured -2 % at 512 img/GPU with the direct 8-B loads.
+        self.bnb_fusion = bnb_fusion
+        blocks = list(model.blocks())
+        for k, b in enumerate(blocks):
+            b._prev_block = blocks[k - 1] if k > 0 else None
+            b._fuse_bnb = bnb_fusion
+            b._last_bn = None
+            b._bnb_done = False
         self._bind_shadows()
         self._bind_workspace()
 
@@ -100,7 +111,8 @@ class NativeState:
         bns: List[BatchNorm2d] = self.model.batchnorms()
         sizes = [bn.num_features for bn in bns]
         S = _lib.STAT_SLOTS
-        per = [(2 * S + 3) * c for c in sizes]          # stats slab + bwd scratch (zeroed)
+        nbw = _lib.kernels().imk_bn_bwd_scratch_floats(1)
+        per = [(2 * S + nbw) * c for c in sizes]        # stats slab + bwd slab/scratch (zeroed)
         self.zero_ws = torch.zeros(sum(per), dtype=torch.float32, device=self.device)
         self.save_ws = torch.zeros(sum(4 * c for c in sizes), dtype=torch.float32, device=self.device)
         o = so = 0
@@ -108,11 +120,11 @@ class NativeState:
         for i, bn in enumerate(bns):
             c = bn.num_features
             slab = self.zero_ws[o:o + 2 * S * c].view(S, 2, c)
-            scratch = self.zero_ws[o + 2 * S * c:o + (2 * S + 3) * c]
+            scratch = self.zero_ws[o + 2 * S * c:o + (2 * S + nbw) * c]
             stats = self.save_ws[so:so + 2 * c]
             save = self.save_ws[so + 2 * c:so + 4 * c]
             bn.work = BNWork(slab, stats, save, scratch)
-            o += (2 * S + 3) * c
+            o += (2 * S + nbw) * c
             so += 4 * c
             d = descs[i]
             d.sums, d.rmean, d.rvar = stats.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr()

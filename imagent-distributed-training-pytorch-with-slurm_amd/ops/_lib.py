@@ -84,6 +84,8 @@ class IGemmArgs(C.Structure):
         ("YH", C.c_int), ("YW", C.c_int), ("sY", C.c_int), ("oy", C.c_int), ("ox", C.c_int),
         ("ldy", C.c_int),
         ("flags", C.c_int),
+        ("bnx", C.c_void_p), ("bny", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
+        ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
     ]
 
 
@@ -121,6 +123,7 @@ def _declare(name: str, lib) -> None:
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
+            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
@@ -135,7 +138,7 @@ def _declare(name: str, lib) -> None:
             "imk_normalize_u8": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_transpose_batched": [vp, i32, i32, vp],
             "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [],
-            "imk_tdesc_size": [],
+            "imk_tdesc_size": [], "imk_bn_bwd_scratch_floats": [i32],
         }
         for fn, args in sigs.items():
             f = getattr(lib, fn)

@@ -12,7 +12,14 @@ The backward is explicit instead of autograd-derived, which lets it
   no extra read/write of a full activation);
 * release each parameter's gradient to the bucketed reducer the moment its
   kernel has been queued (bn3 -> conv3 -> bn2 -> conv2 -> bn1 -> ds -> conv1);
-* skip the ReLU-output read in BN backward (mask recomputed from x).
+* skip the ReLU-output read in BN backward (mask recomputed from x);
+* fold each BatchNorm-backward reduction into the dgrad that produces the
+  BN's upstream gradient (``BNBwdFuse``, conv epilogue IG_BNBWD): the dgrad
+  stores the ReLU-masked gradient and adds sum(g), sum(g*xhat) to the BN's
+  slab, so BN backward is a single apply pass. Inside a block this covers
+  bn1..bnK-1; the block's LAST BN is finished by the NEXT block's first-conv
+  dgrad (the last writer of this block's output gradient, `_prev_block`
+  link), which marks it `_bnb_done`.
 
 It also removes ~6 autograd nodes and their Python dispatch per block.
 """
@@ -21,8 +28,8 @@ from __future__ import annotations
 
 import torch
 
-from .bn import bn_act_backward, bn_act_forward
-from .conv import conv_wgrad, igemm_dgrad, igemm_fwd
+from .bn import bn_act_backward, bn_act_forward, bn_apply_backward
+from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
 def _fwd(conv, h, bn):
@@ -55,6 +62,9 @@ class BlockFn(torch.autograd.Function):
         if ad is not None:
             rows.append(ad.numel() // ad.shape[-1])
         block._bn_rows = rows
+        # what the next block's backward needs to finish this block's last BN
+        block._last_bn = (a, ad, out) if getattr(block, "_fuse_bnb", False) else None
+        block._bnb_done = False
         ctx.block = block
         ctx.save_for_backward(*saved)
         return out
@@ -75,23 +85,47 @@ class BlockFn(torch.autograd.Function):
         H, W = x.shape[1], x.shape[2]
         conv_l, bn_l, _ = pairs[-1]
         ds = block.downsample
+        fuse = getattr(block, "_fuse_bnb", False)
+        premasked = getattr(block, "_bnb_done", False)
         if ds is not None:
-            dA, dAd = bn_act_backward(dout, a_last, ad, out, bn_l, ds[1], 2, True)
+            if premasked:  # dout already masked + reduced by the next block's conv1 dgrad
+                dA, dAd = bn_apply_backward(dout, a_last, ad, bn_l, ds[1], 2)
+            else:
+                dA, dAd = bn_act_backward(dout, a_last, ad, out, bn_l, ds[1], 2, True)
             dconv = ds[0]
             dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw)
             conv_wgrad(dconv, dAd, x)
+        elif premasked:
+            dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1)
+            dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
         else:
             dA, dX = bn_act_backward(dout, a_last, x, out, bn_l, None, 1, True)  # dX = masked dout
+        block._last_bn = None
+        block._bnb_done = False
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             h_in = inputs[i]
             if i > 0:
+                bn_prev = pairs[i - 1][1]
+                fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 dH = igemm_dgrad(dA, conv.wt_bf16, (h_in.shape[1], h_in.shape[2]), conv.stride, conv.padding,
-                                 conv.kh, conv.kw)
+                                 conv.kh, conv.kw, bnb=fz)
                 conv_wgrad(conv, dA, h_in)
-                dA, _ = bn_act_backward(dH, acts[i - 1], None, None, pairs[i - 1][1], None, 0, True)
+                if fz is not None:
+                    dA, _ = bn_apply_backward(dH, acts[i - 1], None, bn_prev, None, 0)
+                else:
+                    dA, _ = bn_act_backward(dH, acts[i - 1], None, None, bn_prev, None, 0, True)
             else:
+                prev = getattr(block, "_prev_block", None)
+                fz = None
+                if fuse and prev is not None and prev._last_bn is not None:
+                    pa, pad_, pout = prev._last_bn
+                    pbn = prev.convs_bns()[-1][1]
+                    pds = prev.downsample
+                    fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
-                            accumulate=True)
+                            accumulate=True, bnb=fz)
                 conv_wgrad(conv, dA, h_in)
+                if fz is not None:
+                    prev._bnb_done = True
         return dX, None

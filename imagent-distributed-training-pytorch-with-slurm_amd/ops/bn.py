@@ -84,6 +84,31 @@ def bn_act_backward(dy: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor
     return dx, (dres if mode == 1 else dx2)
 
 
+def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2,
+                      mode: int) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Backward of act(bn(x) [+ res | + bn2(x2)]) for a gradient ``g`` that its
+    producing dgrad already ReLU-masked and reduced into ``bn.work.scratch``
+    (``ops.conv.BNBwdFuse``): one fold + one streaming apply pass.
+    Returns (dx, dx2 | None); for mode 1 the residual-branch gradient is g."""
+    w = bn.work
+    C = x.shape[-1]
+    R = x.numel() // C
+    dx = torch.empty_like(x)
+    dx2 = torch.empty_like(x2) if mode == 2 else None
+    _lib.check(_lib.kernels().imk_bn_bwd_apply(
+        g.data_ptr(), x.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(), _lib.ptr(x2),
+        bn2.work.save.data_ptr() if mode == 2 else 0, bn2.weight.data_ptr() if mode == 2 else 0,
+        w.scratch.data_ptr(), dx.data_ptr(), _lib.ptr(dx2), bn.weight.grad.data_ptr(),
+        bn.bias.grad.data_ptr(), bn2.weight.grad.data_ptr() if mode == 2 else 0,
+        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _lib.stream_ptr()), "bn bwd apply")
+    notify_ready(bn.weight)
+    notify_ready(bn.bias)
+    if mode == 2:
+        notify_ready(bn2.weight)
+        notify_ready(bn2.bias)
+    return dx, dx2
+
+
 class BNActFn(torch.autograd.Function):
     """y = act(bn(x) [+ res | + bn2(x2)]) as an autograd node (stem, tests)."""
 

@@ -144,6 +144,7 @@ def test_conv_fwd_bias_fp32_out():
 @pytest.mark.parametrize("C", [64, 256, 2048])
 def test_bn_fwd_bwd(mode, C):
     from imagent_amd.models.resnet import BatchNorm2d, BNWork
+    from imagent_amd.ops import _lib
     from imagent_amd.ops.bn import BNActFn
     torch.manual_seed(2)
     N, H = 4, 7
@@ -162,8 +163,9 @@ def test_bn_fwd_bwd(mode, C):
     for m, t in ((bn, x), (bn2, x2)):
         slab = torch.zeros(32, 2, C, device=DEV)
         slab[3] = torch.stack([t.float().sum((0, 1, 2)), (t.float() ** 2).sum((0, 1, 2))])
+        nbw = _lib.kernels().imk_bn_bwd_scratch_floats(C)
         m.work = BNWork(slab, torch.zeros(2, C, device=DEV), torch.zeros(2, C, device=DEV),
-                        torch.zeros(3, C, device=DEV))
+                        torch.zeros(nbw, device=DEV))
     xa = x.clone().requires_grad_(True)
     x2a = x2.clone().requires_grad_(True)
     y = BNActFn.apply(xa, x2a if mode else None, bn, bn2 if mode == 2 else None, mode, True)

@@ -85,3 +85,42 @@ def test_hip_vs_torch_forward_backward(arch, fused):
         with torch.autocast("cuda", dtype=torch.bfloat16):
             ebf = rel(ref_bf(xr).float(), ref(xr))
         assert rel(model(x), ref(xr)) < max(5e-2, 2.0 * ebf)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_fused_bn_backward_matches_unfused(arch):
+    """IG_BNBWD (BN-backward reductions in the dgrad epilogue, cross-block
+    hand-off) vs the separate reduce pass. Summation order differs, and a
+    random-init network's bf16 backward amplifies that (~15 % between the two
+    paths on the stem at this tiny batch), so both are held to the fp32
+    oracle: the fused path may not be further from it than the unfused one."""
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native import bind_native
+    torch.manual_seed(3)
+    base = resnet.build(arch, num_classes=1000)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(8, 48, 48, 4, device=DEV, generator=g).to(torch.bfloat16)
+    x[..., 3] = 0
+    lab = torch.randint(0, 1000, (8,), device=DEV, generator=g)
+    grads = []
+    for fuse in (False, True):
+        model = copy.deepcopy(base)
+        st = bind_native(model, DEV)
+        for b in model.blocks():
+            b._fuse_bnb = fuse
+        model.train()
+        st.arena.zero_grad()
+        F.cross_entropy(model(x), lab).backward()
+        grads.append({n: p.grad.float().clone() for n, p in model.named_parameters()})
+    ref = copy.deepcopy(base).to(DEV)
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    ref.train()
+    F.cross_entropy(ref(x[..., :3].float().permute(0, 3, 1, 2).contiguous()), lab).backward()
+    bad = []
+    for n, p in ref.named_parameters():
+        e_u, e_f = rel(grads[0][n], p.grad), rel(grads[1][n], p.grad)
+        if e_f > max(0.05, 1.3 * e_u + 0.03):
+            bad.append((n, e_u, e_f))
+    assert not bad, bad
