@@ -52,6 +52,7 @@ def main(argv=None):
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
+    ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
     a = ap.parse_args(argv)
 
     from imagent_amd.data.loader import InputTransform
@@ -77,7 +78,7 @@ def main(argv=None):
     native = None
     if a.kernels == "hip":
         from imagent_amd.models.native import bind_native
-        native = bind_native(model, dev, order)
+        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion))
         arena = native.arena
     else:
         model.to(dev)

@@ -47,6 +47,8 @@
 // 32-slot fp32 slab. Tiles are XCD-remapped so concurrently running channel
 // tiles of one pixel panel share an XCD's L2.
 
+#include <algorithm>
+
 #include "common.h"
 
 struct IGemmArgs {
@@ -79,6 +81,8 @@ struct IGemmArgs {
 #define IG_ACCUM 8     // out += result (bf16 out only): fused gradient accumulation
 #define IG_REGSTAGE 16 // force the register-staged main loop (A/B testing)
 #define IG_BNBWD 32    // epilogue = ReLU mask + BatchNorm-backward reductions (slab [32][3][Nout])
+#define IG_EPI_LDS 64  // LDS-staged coalesced epilogue (default for IG_BNBWD)
+#define IG_EPI_DIRECT 128  // direct register epilogue even for IG_BNBWD (A/B testing)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes
@@ -333,13 +337,192 @@ __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&a
     }
 }
 
-template <int FN, int FM, bool BNB>
+template <int FN, int FM, int EPI>
 __device__ __forceinline__ void epilogue(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb, int lane,
                                          float* st) {
-    if (BNB)
+    if (EPI == 1)
         epilogue_bnb<FN, FM>(a, acc, nb, mb, lane, st);
     else
         epilogue_tile<FN, FM>(a, acc, nb, mb, lane, st);
+}
+
+// ---------------------------------------------------- LDS-staged epilogue
+// (EPI 2; bf16 output, no bias / ReLU / fp32; one tile per block so the
+// whole stage ring is free once the main loop has drained.)
+// The block's BM x BN accumulator tile is rounded to bf16 into LDS (row pitch
+// BN*2 + 16 B), then re-read as 16-B row chunks: consecutive lanes cover
+// consecutive channels of one output pixel, so every global access of the
+// epilogue -- the store, the IG_ACCUM read-back, and the IG_BNBWD reads of
+// x, y / x2 -- is a coalesced row segment of BN*2 bytes instead of sixteen
+// 32-B pieces per wave instruction. Statistics (forward: sum, sumsq; BNBWD:
+// sum(g*xhat), sum(g) [, sum(g*xhat2)]) are per thread over its 8 channels,
+// folded across the threads sharing a channel chunk in LDS, then one atomic
+// per channel and quantity into the block's slab slot.
+// (IG_ACCUM adds the old value to the bf16-rounded new one: one extra
+// rounding of the new term versus the direct epilogue.)
+template <int BM, int BN, int NT, int FN, int FM>
+__device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], char* smem, int m0,
+                                             int n0, int wrow0, int wcol0, int lane, int tid, float* st) {
+    constexpr int P = BN * 2 + 16;  // LDS row pitch, bytes
+    constexpr int CPR = BN / 8;     // 16-B chunks per row
+    constexpr int RG = NT / CPR;    // rows processed concurrently (row groups)
+    constexpr int NQ = BM / RG;     // chunks per thread
+    static_assert(NT % CPR == 0 && BM % RG == 0, "epilogue split");
+    const bool accum = a.flags & IG_ACCUM, bnb = a.flags & IG_BNBWD;
+    const bool has_y = bnb && a.bny, has_x2 = bnb && a.bnx2;
+    // (1) fragments -> LDS (8 B per lane: 4 channels of one pixel)
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+            const int row = wrow0 + j * 16 + (lane & 15), col = wcol0 + i * 16 + (lane >> 4) * 4;
+            const f32x4 v = acc[i][j];
+            *reinterpret_cast<u32x2*>(smem + row * P + col * 2) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+        }
+    __syncthreads();
+    // (2) row chunks: thread -> fixed channel chunk cc, rows rg + RG*q
+    const int cc = tid % CPR, rg = tid / CPR;
+    const int n = n0 + cc * 8;
+    const bool nok = n < a.Nout;  // Nout % 8 == 0 on this path
+    float mean[8], rstd[8], sc[8], sh[8], m2[8], r2[8];
+    if (bnb && nok) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 mu = *reinterpret_cast<const f32x4*>(a.bnsave + n + 4 * h);
+            const f32x4 rs = *reinterpret_cast<const f32x4*>(a.bnsave + a.Nout + n + 4 * h);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                mean[4 * h + r] = mu[r];
+                rstd[4 * h + r] = rs[r];
+            }
+            if (!has_y) {
+                const f32x4 g = *reinterpret_cast<const f32x4*>(a.bngamma + n + 4 * h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(a.bnbeta + n + 4 * h);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sc[4 * h + r] = g[r] * rs[r];
+                    sh[4 * h + r] = b[r] - mu[r] * sc[4 * h + r];
+                }
+            }
+            if (has_x2) {
+                const f32x4 mu2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + n + 4 * h);
+                const f32x4 rs2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + a.Nout + n + 4 * h);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    m2[4 * h + r] = mu2[r];
+                    r2[4 * h + r] = rs2[r];
+                }
+            }
+        }
+    }
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
+    const int ohw = a.OH * a.OW;
+    constexpr int QB = 4;  // chunks whose global reads are issued together
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += QB) {
+        long e[QB];
+        u32x4 xo[QB], yo[QB], x2o[QB], oo[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+            const int row = rg + RG * (q0 + u);
+            const int m = m0 + row;
+            e[u] = -1;
+            if (q0 + u < NQ && m < a.M && nok) {
+                const int img = m / ohw, rem = m - img * ohw;
+                const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                e[u] = (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy + n;
+                if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
+                if (bnb) {
+                    xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                    if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
+                    if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+            if (e[u] < 0) continue;
+            const int row = rg + RG * (q0 + u);
+            const u32x4 t = *reinterpret_cast<const u32x4*>(smem + row * P + cc * 16);
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = lo_bf(t[k]);
+                v[2 * k + 1] = hi_bf(t[k]);
+                if (accum) {
+                    v[2 * k] += lo_bf(oo[u][k]);
+                    v[2 * k + 1] += hi_bf(oo[u][k]);
+                }
+            }
+            float xv[8];
+            if (bnb) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    xv[2 * k] = lo_bf(xo[u][k]);
+                    xv[2 * k + 1] = hi_bf(xo[u][k]);
+                }
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const bool keep = has_y ? ((c & 1 ? hi_bf(yo[u][c >> 1]) : lo_bf(yo[u][c >> 1])) > 0.f)
+                                            : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
+                    if (!keep) v[c] = 0.f;
+                }
+            }
+            u32x4 o;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+            *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[u]) = o;
+            if (st) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // statistics of the stored (bf16) values
+                    v[2 * k] = lo_bf(o[k]);
+                    v[2 * k + 1] = hi_bf(o[k]);
+                }
+                if (bnb) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        s1[c] += v[c] * ((xv[c] - mean[c]) * rstd[c]);
+                        s2[c] += v[c];
+                    }
+                    if (has_x2) {
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) {
+                            const float x2 = c & 1 ? hi_bf(x2o[u][c >> 1]) : lo_bf(x2o[u][c >> 1]);
+                            s3[c] += v[c] * ((x2 - m2[c]) * r2[c]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        s1[c] += v[c];
+                        s2[c] += v[c] * v[c];
+                    }
+                }
+            }
+        }
+    }
+    if (!st) return;
+    // (3) fold the RG row groups per channel in LDS, one atomic per channel and quantity
+    const int nq = has_x2 ? 3 : 2;
+    float* red = reinterpret_cast<float*>(smem);  // [nq][RG][BN]
+    __syncthreads();  // everyone is done reading the tile
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        red[(0 * RG + rg) * BN + cc * 8 + c] = s1[c];
+        red[(1 * RG + rg) * BN + cc * 8 + c] = s2[c];
+        if (has_x2) red[(2 * RG + rg) * BN + cc * 8 + c] = s3[c];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nq * BN; idx += NT) {
+        const int qi = idx / BN, ch = idx - qi * BN;
+        if (n0 + ch >= a.Nout) continue;
+        float sum = 0.f;
+#pragma unroll 8
+        for (int g = 0; g < RG; ++g) sum += red[(qi * RG + g) * BN + ch];
+        atomicAdd(st + qi * a.Nout + n0 + ch, sum);
+    }
 }
 
 // MFMA over one 64-deep stage held in LDS (rows of 128 B, chunk-swizzled)
@@ -366,7 +549,7 @@ __device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* b
 // ======================================================= LDS-DMA ring kernel
 // NW waves per block (4: two blocks per CU; 8: one big-tile block per CU,
 // two waves per SIMD, fewer L2->LDS bytes per MFMA FLOP)
-template <int BM, int BN, int WN, int NS, int MODE, int NW, bool BNB>  // MODE 0: C%64==0, 1: C%8==0
+template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI>  // MODE 0: C%64==0, 1: C%8==0
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -500,7 +683,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         if (++kt == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-            epilogue<FN, FM, BNB>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
+            if (EPI == 2) break;  // one tile per block (host): staged epilogue after the loop
+            epilogue<FN, FM, EPI>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -509,10 +693,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
             ++tj;
         }
     }
+    if (EPI == 2) {  // every stage has landed and (barrier) every wave is done reading the ring
+        __syncthreads();
+        const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
+        epilogue_lds<BM, BN, NW * 64, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st);
+    }
 }
 
 // ================================================= register-staged kernel
-template <int BM, int BN, int WN, int MODE, bool BNB>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
+template <int BM, int BN, int WN, int MODE, int EPI>  // MODE 0: C%64==0, 1: C%8==0, 2: stem row segments
 __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
     constexpr int WM = 4 / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -659,7 +848,8 @@ __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
         if (kt + 1 == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
-            epilogue<FN, FM, BNB>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
+            if (EPI == 2) break;  // one tile per block (host): staged epilogue after the loop
+            epilogue<FN, FM, EPI>(a, acc, n0 + wn * TN + (lane >> 4) * 4, m0 + wm * TM + fr, lane, st);
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -671,6 +861,11 @@ __global__ __launch_bounds__(256, 2) void igemm_rs_kernel(const IGemmArgs a) {
         }
         if (has_next) store_stage(buf ^ 1);
         __syncthreads();
+    }
+    if (EPI == 2) {
+        __syncthreads();
+        const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
+        epilogue_lds<BM, BN, 256, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st);
     }
 }
 
@@ -685,6 +880,13 @@ int resident_blocks(KernelT kern, size_t lds, int threads = 256) {
     return per_cu * cus;
 }
 
+// LDS bytes the staged epilogue needs: the bf16 tile, then the statistics fold
+inline size_t epi_lds_bytes(int BM, int BN, int NT) {
+    const size_t tile = (size_t)BM * (BN * 2 + 16);
+    const size_t red = (size_t)3 * (NT / (BN / 8)) * BN * sizeof(float);
+    return std::max(tile, red);
+}
+
 // persistent only where it pays: tiles with few K-stages (memory-bound 1x1
 // convs) overlap the next tile's loads with this tile's epilogue; long-K tiles
 // keep one tile per block (the hardware refills CUs without a tail)
@@ -692,27 +894,31 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4, bool BNB = false>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-    const size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
+    size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
+    if (EPI == 2) lds = std::max(lds, epi_lds_bytes(BM, BN, NW * 64));
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, BNB>, lds, NW * 64);
+    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI>, lds, NW * 64);
     const int nk = (a.nth * a.ntw * a.C + BK - 1) / BK;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, BNB>), dim3(grid_size(ntiles, nk, resident)),
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI>),
+                       dim3(EPI == 2 ? ntiles : grid_size(ntiles, nk, resident)),
                        dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
-template <int BM, int BN, int WN, int MD, bool BNB = false>
+template <int BM, int BN, int WN, int MD, int EPI = 0>
 int launch_rs(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-    const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
+    size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(bf16_t);
+    if (EPI == 2) lds = std::max(lds, epi_lds_bytes(BM, BN, 256));
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_rs_kernel<BM, BN, WN, MD, BNB>, lds);
+    if (resident == 0) resident = resident_blocks(igemm_rs_kernel<BM, BN, WN, MD, EPI>, lds);
     const int K = MD == 2 ? a.nth * 32 : a.nth * a.ntw * a.C;
-    hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD, BNB>), dim3(grid_size(ntiles, (K + BK - 1) / BK, resident)),
+    hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD, EPI>),
+                       dim3(EPI == 2 ? ntiles : grid_size(ntiles, (K + BK - 1) / BK, resident)),
                        dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
@@ -753,18 +959,26 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         if (t8 >= 192) tile = 8;
     }
     const bool bnb = a.flags & IG_BNBWD;
-    if (bnb) {  // backward-data convs only: the tiles the auto choice makes, fused epilogue
+    const bool lds_ok = !(a.flags & (IG_OUT_F32 | IG_RELU)) && !a.bias && a.Nout % 8 == 0 && a.ldy % 8 == 0;
+    // staged epilogue: always with the fused BN backward; otherwise for long-K
+    // tiles (non-persistent anyway, +5-10 % measured) -- short-K memory-bound
+    // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
+    const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
+                         (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
+    if (bnb || use_lds) {  // the tiles the auto choice makes, with a fused / staged epilogue
         if (regstage || (tile != 2 && tile != 8)) {
             if (tile != 2) tile = 4;
-#define IG_RSB(BM_, BN_, WN_) \
-    (md == 0 ? launch_rs<BM_, BN_, WN_, 0, true>(a, st) : launch_rs<BM_, BN_, WN_, 1, true>(a, st))
-            return tile == 2 ? IG_RSB(128, 128, 2) : IG_RSB(128, 64, 1);
+#define IG_RSB(BM_, BN_, WN_, E_) \
+    (md == 0 ? launch_rs<BM_, BN_, WN_, 0, E_>(a, st) : launch_rs<BM_, BN_, WN_, 1, E_>(a, st))
+            if (use_lds) return tile == 2 ? IG_RSB(128, 128, 2, 2) : IG_RSB(128, 64, 1, 2);
+            return tile == 2 ? IG_RSB(128, 128, 2, 1) : IG_RSB(128, 64, 1, 1);
 #undef IG_RSB
         }
-#define IG_DB(BM_, BN_, WN_, NS_, NW_)                                                  \
-    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, true>(a, st)                       \
-             : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, true>(a, st))
-        return tile == 8 ? IG_DB(256, 256, 2, 2, 8) : IG_DB(128, 128, 2, 2, 4);
+#define IG_DB(BM_, BN_, WN_, NS_, NW_, E_)                                                  \
+    (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, E_>(a, st)                       \
+             : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, E_>(a, st))
+        if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
+        return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB
     }
     if (regstage) {

@@ -45,10 +45,15 @@ def _base_args(x_ptr, w_ptr, y_ptr, N, H, W, Cin, OH, OW, Nout, ldb, sA) -> _lib
     return a
 
 
+# epilogue choice: 0 auto (LDS-staged for fused BN backward, else direct),
+# 1 direct register epilogue, 2 LDS-staged coalesced epilogue
+_EPI_FLAGS = {0: 0, 1: 128, 2: 64}
+
+
 def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
               stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
-              tile: int = 0, stem: bool = False) -> torch.Tensor:
+              tile: int = 0, stem: bool = False, epi: int = 0) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` [2, Co].
 
@@ -67,7 +72,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = KH, KW, -pad, 1, -pad, 1
     a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
-    a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0)
+    a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0) | _EPI_FLAGS[epi]
     if bias is not None:
         a.bias = bias.data_ptr()
     if stats is not None:
@@ -78,7 +83,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
 
 def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
                 KH: int, KW: int, out: Optional[torch.Tensor] = None,
-                accumulate: bool = False, tile: int = 0, bnb: Optional["BNBwdFuse"] = None) -> torch.Tensor:
+                accumulate: bool = False, tile: int = 0, bnb: Optional["BNBwdFuse"] = None,
+                epi: int = 0) -> torch.Tensor:
     """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci,KH,KW,Co]).
 
     Stride 1: one gather-GEMM launch with the taps mirrored.
@@ -120,7 +126,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = 8 if accumulate else 0
+            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi]
             if bnb is not None:
                 bnb.fill(a)
             _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
     ap.add_argument("--no-stats", action="store_true", help="forward without the fused BN statistics")
+    ap.add_argument("--epi", type=int, default=0, help="0 auto, 1 direct, 2 LDS-staged epilogue")
     ap.add_argument("--tiles", default=None, help="comma list of explicit tile ids to time for fwd/dgrad")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
@@ -89,8 +90,8 @@ def main():
         dw = torch.zeros(Co, k, 32, device=dev) if stem else torch.zeros(Co, k, k, Cin, device=dev)
         stats = None if a.no_stats else torch.zeros(32, 2, Co, device=dev)
         flops = 2.0 * B * OH * OH * Co * k * k * Ci
-        t_f = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, stem=stem))
-        t_d = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k)) if not stem else 0.0
+        t_f = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, stem=stem, epi=0 if stem else a.epi))
+        t_d = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, epi=a.epi)) if not stem else 0.0
         t_w = timeit(lambda: igemm_wgrad(dy, x, dw, s, p, k, k, stem=stem))
         roof = (x.numel() * 2 + dy.numel() * 2 + w.numel() * 2) / 6e12 * 1e6
         line = (f"{Ci:5d} {H:4d} {Co:5d} {k} {s} | {cnt:3d} | {t_f:8.1f} {flops / t_f / 1e6:6.0f} {roof:6.1f} | "

@@ -99,6 +99,35 @@ def test_conv_explicit_tiles(tile, shape):
     assert rel(nchw(dx), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [0, 2, 4, 8])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 512, 1, 1, 0),
+                                   (5, 96, 7, 64, 1, 1, 0)])
+def test_conv_lds_epilogue(tile, shape):
+    """LDS-staged coalesced epilogue: forward + statistics, dgrad, dgrad accumulate."""
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(4)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = bf(torch.randn(Co, Ci, k, k, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5)
+    xr = x.float().requires_grad_(True)
+    yr = F.conv2d(xr, w.float(), None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(nhwc(x), nhwc(w), s, p, k, k, stats=slab, tile=tile, epi=2)
+    assert rel(nchw(y), yr) < 1e-2
+    yb = nchw(y).float()
+    assert rel(slab.sum(0)[0], yb.sum((0, 2, 3))) < 1e-3
+    assert rel(slab.sum(0)[1], (yb * yb).sum((0, 2, 3))) < 1e-3
+    wt = w.permute(1, 2, 3, 0).contiguous()
+    dx = igemm_dgrad(nhwc(g), wt, (H, H), s, p, k, k, tile=tile, epi=2)
+    assert rel(nchw(dx), xr.grad) < 1e-2
+    base = bf(torch.randn(N, H, H, Ci, device=DEV))
+    acc = base.clone()
+    igemm_dgrad(nhwc(g), wt, (H, H), s, p, k, k, out=acc, accumulate=True, tile=tile, epi=2)
+    assert rel(acc.float() - base.float(), nhwc(xr.grad)) < 2e-2
+
+
 def test_stem_row_segment_conv():
     """7x7/s2 stem: 4-channel NHWC input, [Co][KH][32] weight rows (fwd + wgrad)."""
     from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
