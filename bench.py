@@ -53,6 +53,8 @@ def main(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward")
     a = ap.parse_args(argv)
 
     from imagent_amd.data.loader import InputTransform
@@ -78,7 +80,7 @@ def main(argv=None):
     native = None
     if a.kernels == "hip":
         from imagent_amd.models.native import bind_native
-        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion))
+        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8")
         arena = native.arena
     else:
         model.to(dev)
@@ -129,7 +131,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.dtype == "bf16" else "fp8 (e4m3 forward convs, bf16 backward)",
             "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
                     "random-init weights)",
             "config": {

@@ -66,11 +66,14 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     const float* __restrict__ beta, const bf16_t* __restrict__ x2, const float* __restrict__ sums2,
     const float* __restrict__ gamma2, const float* __restrict__ beta2, bf16_t* __restrict__ y,
     float* __restrict__ save, float* __restrict__ save2, long R, int C, float inv_cnt, float eps,
-    int eval) {
+    int eval, uint32_t* __restrict__ y8, const int* __restrict__ exp8, float* __restrict__ amax8) {
     const int cpr = C / 8;                // chunks per row
     const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
     const int tid = threadIdx.x;
-    if (tid >= rpb * cpr) return;
+    // fp8 copy of the output for the next conv (delayed-scaled e4m3, fp8.hip)
+    const float q8 = y8 ? ldexpf(1.f, -exp8[0]) : 0.f;
+    float m8 = 0.f;
+    if (tid >= rpb * cpr) return;  // (host: with y8, every lane is active -- C/8 divides 256)
     const int ch = tid % cpr, c0 = ch * 8;
     float sc[8], sh[8], sc2[8], sh2[8];
 #pragma unroll
@@ -129,7 +132,23 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
                 v[u].v[i] = RELU ? fmaxf(o, 0.f) : o;
             }
             st8(y + (size_t)r * C + c0, v[u]);
+            if (y8) {
+                // quantise the bf16-rounded output the bf16 consumers see
+                float w[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    w[i] = bf2f(f2bf(v[u].v[i]));
+                    m8 = fmaxf(m8, fabsf(w[i]));
+                }
+                reinterpret_cast<u32x2*>(y8)[((size_t)r * C + c0) / 8] =
+                    u32x2{pack4_fp8(w[0] * q8, w[1] * q8, w[2] * q8, w[3] * q8),
+                          pack4_fp8(w[4] * q8, w[5] * q8, w[6] * q8, w[7] * q8)};
+            }
         }
+    }
+    if (y8) {
+        m8 = wave_max(m8);
+        if ((tid & 63) == 0) atomic_max_pos(amax8, m8);
     }
 }
 
@@ -361,18 +380,20 @@ int grid_for(long R, int C) {
 }  // namespace
 
 // mode: 0 plain, 1 + identity residual (x2), 2 + second BN branch (x2, sums2, gamma2, beta2)
+// y8 (optional): e4m3 copy of y quantised with 2^-exp8[0]; amax8 receives max |y|
 IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, const float* beta,
                           const void* x2, const float* sums2, const float* gamma2, const float* beta2,
                           void* y, float* save, float* save2, long R, int C, int mode, int relu,
-                          float eps, int eval, void* stream) {
+                          float eps, int eval, void* y8, const int* exp8, float* amax8, void* stream) {
     if (C % 8 || C > 2048) return -100;
+    if (y8 && (256 % (C / 8) || !exp8 || !amax8)) return -102;
     const float inv_cnt = 1.f / (float)R;
     const int grid = grid_for(R, C);
     hipStream_t st = (hipStream_t)stream;
 #define L(M, RL)                                                                                   \
     hipLaunchKernelGGL((bn_fwd_kernel<M, RL>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
                        gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, \
-                       R, C, inv_cnt, eps, eval)
+                       R, C, inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8)
     if (mode == 0) { if (relu) L(0, true); else L(0, false); }
     else if (mode == 1) { if (relu) L(1, true); else L(1, false); }
     else { if (relu) L(2, true); else L(2, false); }

@@ -11,6 +11,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 #define WAVE 64
 #define LDS_PTR(T) __attribute__((address_space(3))) T*
@@ -60,3 +61,21 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
         hipError_t e_ = hipGetLastError();         \
         if (e_ != hipSuccess) return (int)e_;      \
     } while (0)
+
+// ---- fp8 (OCP e4m3, gfx950 v_cvt_pk_fp8_f32), saturating to +-448
+constexpr float E4M3_MAX = 448.f;
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+    a = fminf(fmaxf(a, -E4M3_MAX), E4M3_MAX);
+    b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
+    c = fminf(fmaxf(c, -E4M3_MAX), E4M3_MAX);
+    d = fminf(fmaxf(d, -E4M3_MAX), E4M3_MAX);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+    return (uint32_t)w;
+}
+
+__device__ __forceinline__ void atomic_max_pos(float* p, float v) {
+    // v >= 0: IEEE order of non-negative floats == order of their bit patterns
+    atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}

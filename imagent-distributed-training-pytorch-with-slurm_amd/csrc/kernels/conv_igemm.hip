@@ -73,6 +73,11 @@ struct IGemmArgs {
     const float* bnbeta;
     const bf16_t* bnx2;    // second BN branch input (downsample), or null
     const float* bnsave2;
+    // IG_FP8: X and Wk hold e4m3 values x*2^-ex, w*2^-ew; the per-tensor
+    // exponents live on the device (delayed scaling, no host sync) and enter
+    // the MFMA as E8M0 scales 127 + e
+    const int* xexp;
+    const int* wexp;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
@@ -83,6 +88,7 @@ struct IGemmArgs {
 #define IG_BNBWD 32    // epilogue = ReLU mask + BatchNorm-backward reductions (slab [32][3][Nout])
 #define IG_EPI_LDS 64  // LDS-staged coalesced epilogue (default for IG_BNBWD)
 #define IG_EPI_DIRECT 128  // direct register epilogue even for IG_BNBWD (A/B testing)
+#define IG_FP8 256     // fp8 e4m3 operands (forward convs; block-scaled MFMA)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes
@@ -546,10 +552,43 @@ __device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* b
     }
 }
 
+// MFMA over one 128-deep fp8 stage (rows of 128 B, chunk-swizzled): one
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair at twice
+// the bf16 MFMA rate. Each lane feeds 32 consecutive k of its row (logical
+// chunks 2g, 2g+1, g = lane>>4) for BOTH operands -- the same lane->k map on
+// A and B, so the hardware's k order inside the instruction cancels out. The
+// per-tensor power-of-two scales ride in the instruction's E8M0 operands:
+// dequantisation is free.
+template <int FN, int FM>
+__device__ __forceinline__ void mfma_stage_fp8(f32x4 (&acc)[FN][FM], const char* bx, const char* bw, int c0, int c1,
+                                               int sw8, int sx8) {
+    i32x8 fw[FN], fx[FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(bw + i * 16 * 128 + c0);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(bw + i * 16 * 128 + c1);
+        fw[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(bx + j * 16 * 128 + c0);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(bx + j * 16 * 128 + c1);
+        fx[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fw[i], fx[j], acc[i][j], 0, 0, 0, sw8, 0, sx8);
+}
+
 // ======================================================= LDS-DMA ring kernel
 // NW waves per block (4: two blocks per CU; 8: one big-tile block per CU,
-// two waves per SIMD, fewer L2->LDS bytes per MFMA FLOP)
-template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI>  // MODE 0: C%64==0, 1: C%8==0
+// two waves per SIMD, fewer L2->LDS bytes per MFMA FLOP).
+// EB = operand element bytes: 2 (bf16, 64-deep stages) or 1 (fp8 e4m3, 128-deep
+// stages, IG_FP8): the DMA moves 16-B chunks either way, the gather differs
+// only in elements per chunk.
+template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI, int EB = 2>  // MODE 0: one tap per stage
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -557,10 +596,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     constexpr int QA = BM / (8 * NW), QB = BN / (8 * NW);  // DMA pieces (8 rows each) per wave per stage
     static_assert(QA >= 1 && QB >= 1 && WM * WN == NW, "tile / wave split");
     constexpr int LPS = QA + QB;               // vmcnt units per stage
-    constexpr int SA = BM * LDK, SB = BN * LDK;  // elements per stage buffer
+    constexpr int KS = 128 / EB;               // k elements per stage (one 128-B LDS row)
+    constexpr int CE = 16 / EB;                // elements per 16-B chunk
+    constexpr int SAB = BM * 128, SBB = BN * 128;  // bytes per stage buffer
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* sX = reinterpret_cast<bf16_t*>(smem);  // [NS][BM][64]
-    bf16_t* sW = sX + NS * SA;                     // [NS][BN][64]
+    char* sX = smem;                 // [NS][BM][128 B]
+    char* sW = smem + NS * SAB;      // [NS][BN][128 B]
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -573,20 +614,22 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     if (lid >= ntiles) return;
     const int my_tiles = (ntiles - lid + G - 1) / G;
     const int K = a.nth * a.ntw * a.C;
-    const int nk = max(1, (K + BK - 1) / BK);
+    const int nk = max(1, (K + KS - 1) / KS);
     const int nstages = my_tiles * nk;
     const int ohw = a.OH * a.OW;
     // this lane's DMA slot: row (lane>>3) of each 8-row piece, physical chunk
     // lane&7 -> logical chunk (lane&7) ^ (row & 7)   (row & 7 == lane >> 3)
     const int lrow = lane >> 3;
     const int lchunk = (lane & 7) ^ lrow;
-    const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_igemm_zero);
+    const char* zero = reinterpret_cast<const char*>(g_igemm_zero);
+    const char* Xb = reinterpret_cast<const char*>(a.X);
+    const char* Wb = reinterpret_cast<const char*>(a.Wk);
 
     // gather state of the tile being LOADED (rows wid*QA*8 + q*8 + lrow)
-    const bf16_t* xrow[QA];
+    const char* xrow[QA];
     int ih0[QA], iw0[QA];
     bool mok[QA];
-    const bf16_t* wrow[QB];
+    const char* wrow[QB];
     bool nok[QB];
     auto setup_rows = [&](int tile) {
         const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
@@ -597,7 +640,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
             const int mm = mok[q] ? m : 0;
             const int img = mm / ohw, rem = mm - img * ohw;
             const int oh = rem / a.OW, ow = rem - oh * a.OW;
-            xrow[q] = a.X + (size_t)img * a.H * a.W * a.C;
+            xrow[q] = Xb + (size_t)img * a.H * a.W * a.C * EB;
             ih0[q] = oh * a.sA;
             iw0[q] = ow * a.sA;
         }
@@ -605,15 +648,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         for (int q = 0; q < QB; ++q) {
             const int n = n0 + (wid * QB + q) * 8 + lrow;
             nok[q] = n < a.Nout;
-            wrow[q] = a.Wk + (size_t)(nok[q] ? n : 0) * a.ldb;
+            wrow[q] = Wb + (size_t)(nok[q] ? n : 0) * a.ldb * EB;
         }
     };
     auto issue = [&](int kt, int buf) {
         int t, c;
-        const int k = kt * BK + lchunk * 8;
+        const int k = kt * KS + lchunk * CE;
         if (MODE == 0) {
-            t = (kt * BK) / a.C;
-            c = kt * BK - t * a.C + lchunk * 8;
+            t = (kt * KS) / a.C;
+            c = kt * KS - t * a.C + lchunk * CE;
         } else {
             t = k / a.C;
             c = k - t * a.C;
@@ -622,19 +665,19 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         const int ti = kok ? t / a.ntw : 0, tj = kok ? t - ti * a.ntw : 0;
         const int dh = a.dh0 + ti * a.dhs, dw = a.dw0 + tj * a.dws;
         const int wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
-        char* dX = reinterpret_cast<char*>(sX + buf * SA) + (wid * QA) * 1024;
-        char* dW = reinterpret_cast<char*>(sW + buf * SB) + (wid * QB) * 1024;
+        char* dX = sX + buf * SAB + (wid * QA) * 1024;
+        char* dW = sW + buf * SBB + (wid * QB) * 1024;
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
             const int ih = ih0[q] + dh, iw = iw0[q] + dw;
             const bool ok = kok && mok[q] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-            const bf16_t* src = ok ? xrow[q] + ((size_t)ih * a.W + iw) * a.C + c : zero;
+            const char* src = ok ? xrow[q] + (((size_t)ih * a.W + iw) * a.C + c) * EB : zero;
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                              (void __attribute__((address_space(3)))*)(dX + q * 1024), 16, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
-            const bf16_t* src = (kok && nok[q]) ? wrow[q] + wtap * a.C + c : zero;
+            const char* src = (kok && nok[q]) ? wrow[q] + ((size_t)wtap * a.C + c) * EB : zero;
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                              (void __attribute__((address_space(3)))*)(dW + q * 1024), 16, 0, 0);
         }
@@ -666,6 +709,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
 
     const int fr = lane & 15;
     const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
+    // fp8: the lane's 32 bytes are logical chunks 2g, 2g+1 of its row (byte offsets)
+    const int f8c0 = ((2 * (lane >> 4)) ^ (fr & 7)) * 16, f8c1 = ((2 * (lane >> 4) + 1) ^ (fr & 7)) * 16;
+    const int sx8 = EB == 1 ? 127 + a.xexp[0] : 127, sw8 = EB == 1 ? 127 + a.wexp[0] : 127;
     int tj = 0, kt = 0;
     for (int s = 0; s < nstages; ++s) {
         // stage s landed for this wave when at most (stages issued after s) x LPS remain
@@ -678,8 +724,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         __builtin_amdgcn_s_barrier();  // ... and for every wave; buffer (s-1)%NS is free
         issue_next();
         const int buf = s % NS;
-        mfma_stage<FN, FM>(acc, sX + buf * SA + (wm * TM + fr) * LDK, sW + buf * SB + (wn * TN + fr) * LDK,
-                           fk0, fk1);
+        if (EB == 1)
+            mfma_stage_fp8<FN, FM>(acc, sX + buf * SAB + (wm * TM + fr) * 128, sW + buf * SBB + (wn * TN + fr) * 128,
+                                   f8c0, f8c1, sw8, sx8);
+        else
+            mfma_stage<FN, FM>(acc, reinterpret_cast<const bf16_t*>(sX + buf * SAB) + (wm * TM + fr) * LDK,
+                               reinterpret_cast<const bf16_t*>(sW + buf * SBB) + (wn * TN + fr) * LDK, fk0, fk1);
         if (++kt == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
@@ -894,17 +944,17 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-    size_t lds = (size_t)NS * (BM + BN) * LDK * sizeof(bf16_t);
+    size_t lds = (size_t)NS * (BM + BN) * 128;
     if (EPI == 2) lds = std::max(lds, epi_lds_bytes(BM, BN, NW * 64));
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI>, lds, NW * 64);
-    const int nk = (a.nth * a.ntw * a.C + BK - 1) / BK;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI>),
-                       dim3(EPI == 2 ? ntiles : grid_size(ntiles, nk, resident)),
-                       dim3(NW * 64), lds, st, a);
+    if (resident == 0)
+        resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB>, lds, NW * 64);
+    const int nk = (a.nth * a.ntw * a.C * EB + 127) / 128;
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB>),
+                       dim3(EPI == 2 ? ntiles : grid_size(ntiles, nk, resident)), dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -939,6 +989,30 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32
         if (a.C != 4 || a.ntw > 8 || a.dhs != 1 || a.dws != 1) return -102;
         return launch_rs<128, 64, 1, 2>(a, st);
+    }
+    if (a.flags & IG_FP8) {  // forward convs on fp8 e4m3 operands
+        if (a.C % 16 != 0 || (a.flags & (IG_BNBWD | IG_ACCUM | IG_OUT_F32)) || a.bias || !a.xexp || !a.wexp)
+            return -105;
+        const int md8 = (a.C % 128) == 0 ? 0 : 1;
+        const int K8 = a.nth * a.ntw * a.C;
+        const bool lds8 = a.Nout % 8 == 0 && a.ldy % 8 == 0 && !(a.flags & (IG_RELU | IG_EPI_DIRECT)) &&
+                          ((a.flags & IG_EPI_LDS) || (K8 + 127) / 128 > 4);
+        if (tile == 0) {
+            tile = a.Nout <= 64 ? 4 : 2;
+            if (a.Nout >= 256 && (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256) >= 192) tile = 8;
+        }
+#define IG_F8(BM_, BN_, WN_, NS_, NW_)                                                                   \
+    (lds8 ? (md8 == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, 2, 1>(a, st)                              \
+                      : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, 2, 1>(a, st))                             \
+          : (md8 == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, 0, 1>(a, st)                              \
+                      : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, 0, 1>(a, st)))
+        switch (tile) {
+            case 2: return IG_F8(128, 128, 2, 2, 4);
+            case 4: return IG_F8(128, 64, 1, 3, 4);
+            case 8: return IG_F8(256, 256, 2, 2, 8);
+            default: return -101;
+        }
+#undef IG_F8
     }
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     const int md = (a.C % BK) == 0 ? 0 : 1;

@@ -32,7 +32,7 @@ def stem_view(t: torch.Tensor, kw: int) -> torch.Tensor:
 
 class NativeState:
     def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None,
-                 bnb_fusion: bool = True):
+                 bnb_fusion: bool = True, fp8: bool = False):
         self.device = torch.device(device)
         named = list(model.named_parameters())
         self.arena = ParamArena(named, self.device, order=order, with_shadow=True)
@@ -51,6 +51,11 @@ class NativeState:
             b._bnb_done = False
         self._bind_shadows()
         self._bind_workspace()
+        self.fp8 = None
+        if fp8:
+            self.fp8 = Fp8State(self)
+            for b in blocks:
+                b._q8 = self.fp8
 
     # ------------------------------------------------------------ shadows
     def _bind_shadows(self):
@@ -99,10 +104,16 @@ class NativeState:
         self.tplan.run()
         s = self.model.conv1
         stem_view(s.w_pad, s.kw)[..., : s.in_channels].copy_(s.w_bf16_real)
+        if getattr(self, "fp8", None) is not None:
+            self.fp8.after_step()
 
     def rebind(self) -> None:
         """After an arena re-layout (bucket rebuild): re-point every shadow."""
         self._bind_shadows()
+        if self.fp8 is not None:
+            self.fp8 = Fp8State(self)
+            for b in self.model.blocks():
+                b._q8 = self.fp8
         self.refresh_shadows(full=True)
 
     # ---------------------------------------------------------- workspace
@@ -146,10 +157,60 @@ class NativeState:
         running_update(self._run_dev, len(self.bns))
 
 
+class Fp8State:
+    """fp8 forward (``--dtype fp8``): e4m3 shadows of the non-stem conv weights
+    (exact per-step scales) and e4m3 copies of every activation a conv reads
+    (delayed per-tensor scales, written by the producing BN / pool). The
+    backward stays bf16 (bf16 weight shadows, bf16 saved activations)."""
+
+    def __init__(self, st: "NativeState"):
+        from ..ops.fp8 import ActScales, WeightQuantizer
+        m = st.model
+        convs = [c for c in m.convs() if c is not m.conv1]
+        self.wq = WeightQuantizer([c.weight for c in convs], st.device)
+        for c, v, i in zip(convs, self.wq.views, range(len(convs))):
+            c.w8 = v.view(c.out_channels, c.kh, c.kw, c.in_channels)
+            c.w8_exp = self.wq.exp[i:i + 1]
+        bns = m.batchnorms()
+        self.slot = {id(bn): i for i, bn in enumerate(bns)}
+        self.pool_slot = len(bns)
+        self.act = ActScales(len(bns) + 1, st.device)
+        self.map = {}
+        self.active = False
+        self.wq.run()
+
+    def after_step(self) -> None:
+        """Masters changed: re-quantise weights; this step's amax -> next exponents."""
+        self.wq.run()
+        self.act.step()
+
+    def begin_forward(self) -> None:
+        self.map.clear()
+        self.active = True
+
+    def end_forward(self) -> None:
+        self.map.clear()
+        self.active = False
+
+    def out_for(self, like: torch.Tensor, slot: int):
+        """(y8 buffer, exponent view, amax view) for a BN / pool output of this shape."""
+        if like.shape[-1] % 16 or 256 % (like.shape[-1] // 8):
+            return None
+        return (torch.empty(like.shape, dtype=torch.uint8, device=like.device), self.act.exp[slot:slot + 1],
+                self.act.amax[slot:slot + 1])
+
+    def register(self, y: torch.Tensor, q8) -> None:
+        if q8 is not None:
+            self.map[y.data_ptr()] = (q8[0], q8[1])
+
+    def lookup(self, y: torch.Tensor):
+        return self.map.get(y.data_ptr())
+
+
 def bind_native(model: ResNet, device, order: Optional[Sequence[int]] = None,
-                bnb_fusion: bool = True) -> NativeState:
+                bnb_fusion: bool = True, fp8: bool = False) -> NativeState:
     model.to(device)
-    st = NativeState(model, device, order, bnb_fusion=bnb_fusion)
+    st = NativeState(model, device, order, bnb_fusion=bnb_fusion, fp8=fp8)
     model.native = st
     model.backend = "hip"
     st.refresh_shadows(full=True)
@@ -182,11 +243,20 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     train = model.training and torch.is_grad_enabled()
     if train:
         st.zero_ws.zero_()
+    q = st.fp8 if (train and st.fused_blocks) else None
+    if q is not None:
+        q.begin_forward()
     rows = []
     y = _conv(x, model.conv1, model.bn1, train)
     rows.append(y.numel() // y.shape[-1])
     y = _bn(y, model.bn1, True, train)
     y = MaxPoolFn.apply(y, 3, 2, 1) if train else maxpool_eval(y, 3, 2, 1)
+    if q is not None:
+        q8 = q.out_for(y, q.pool_slot)
+        if q8 is not None:
+            from ..ops.fp8 import quant_act
+            quant_act(y.detach(), q8[1], q8[2], out=q8[0])
+            q.register(y, q8)
     for b in model.blocks():
         if train and st.fused_blocks:
             y = BlockFn.apply(y, b)
@@ -209,6 +279,8 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
             y = _bn(a, bn, True, train, x2=ad, bn2=dbn, mode=2)
         else:
             y = _bn(a, bn, True, train, x2=idt, mode=1)
+    if q is not None:
+        q.end_forward()
     pooled = AvgPoolFn.apply(y) if train else _avg_eval(y)
     if train:
         logits = LinearFn.apply(pooled, model.fc.weight, model.fc)

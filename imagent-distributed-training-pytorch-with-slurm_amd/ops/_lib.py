@@ -86,7 +86,14 @@ class IGemmArgs(C.Structure):
         ("flags", C.c_int),
         ("bnx", C.c_void_p), ("bny", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
         ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
+        ("xexp", C.c_void_p), ("wexp", C.c_void_p),
     ]
+
+
+class QDesc(C.Structure):
+    """fp8.hip QDesc: one weight tensor of the per-step e4m3 quantisation."""
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("n4", C.c_long), ("exp", C.c_void_p),
+                ("amax", C.c_void_p)]
 
 
 class WgradArgs(C.Structure):
@@ -121,7 +128,8 @@ def _declare(name: str, lib) -> None:
         sigs = {
             "imk_conv_igemm": [C.POINTER(IGemmArgs), i32, vp],
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
-            "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp],
+            "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
+                           vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
@@ -139,6 +147,10 @@ def _declare(name: str, lib) -> None:
             "imk_transpose_batched": [vp, i32, i32, vp],
             "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [],
             "imk_tdesc_size": [], "imk_bn_bwd_scratch_floats": [i32],
+            "imk_quant_fp8": [vp, vp, i64, vp, vp, vp],
+            "imk_fp8_update_exp": [vp, vp, i32, i32, vp],
+            "imk_quant_fp8_weights": [vp, i32, i64, i32, vp],
+            "imk_qdesc_size": [],
         }
         for fn, args in sigs.items():
             f = getattr(lib, fn)
@@ -146,7 +158,8 @@ def _declare(name: str, lib) -> None:
             f.restype = C.c_int
         # ABI guard: the ctypes mirrors must match the compiled structs
         for fn, st in [("imk_igemm_args_size", IGemmArgs), ("imk_wgrad_args_size", WgradArgs),
-                       ("imk_bn_rundesc_size", RunDesc), ("imk_tdesc_size", TDesc)]:
+                       ("imk_bn_rundesc_size", RunDesc), ("imk_tdesc_size", TDesc),
+                       ("imk_qdesc_size", QDesc)]:
             n = getattr(lib, fn)()
             if n != C.sizeof(st):
                 raise RuntimeError(f"{fn}: native {n} B != ctypes {C.sizeof(st)} B - rebuild")

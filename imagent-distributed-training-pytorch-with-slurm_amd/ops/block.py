@@ -37,25 +37,42 @@ def _fwd(conv, h, bn):
                      stats=bn.work.slab, stem=getattr(conv, "stem", False))
 
 
+def _fwd8(conv, h, h8, bn):
+    """fp8 forward (``Fp8State``) when the input has an e4m3 copy, else bf16."""
+    if h8 is None or conv.in_channels % 16:
+        return _fwd(conv, h, bn)
+    return igemm_fwd(h8[0], conv.w8, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work.slab,
+                     fp8=(h8[1], conv.w8_exp))
+
+
 class BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block):
         pairs = block.convs_bns()
+        q = getattr(block, "_q8", None)  # Fp8State or None
+        if q is not None and not q.active:
+            q = None  # not inside a forward_hip training pass
+        x8 = q.lookup(x) if q is not None else None
         saved = [x]
-        h = x
+        h, h8 = x, x8
         for conv, bn, _ in pairs[:-1]:
-            a = _fwd(conv, h, bn)
-            h = bn_act_forward(a, None, bn, None, 0, True)
+            a = _fwd8(conv, h, h8, bn)
+            q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
+            h = bn_act_forward(a, None, bn, None, 0, True, q8=q8)
+            h8 = (q8[0], q8[1]) if q8 is not None else None
             saved += [a, h]
         conv, bn, _ = pairs[-1]
-        a = _fwd(conv, h, bn)
+        a = _fwd8(conv, h, h8, bn)
         ds = block.downsample
+        q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
         if ds is not None:
-            ad = _fwd(ds[0], x, ds[1])
-            out = bn_act_forward(a, ad, bn, ds[1], 2, True)
+            ad = _fwd8(ds[0], x, x8, ds[1])
+            out = bn_act_forward(a, ad, bn, ds[1], 2, True, q8=q8)
         else:
             ad = None
-            out = bn_act_forward(a, x, bn, None, 1, True)
+            out = bn_act_forward(a, x, bn, None, 1, True, q8=q8)
+        if q is not None:
+            q.register(out, q8)
         saved += [a, ad, out]
         # rows seen by each BN (module order: bn1..bnK, downsample.1) for the running-stat update
         rows = [t.numel() // t.shape[-1] for t in saved[1:-3:2]] + [a.numel() // a.shape[-1]]

@@ -53,12 +53,16 @@ _EPI_FLAGS = {0: 0, 1: 128, 2: 64}
 def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
               stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
-              tile: int = 0, stem: bool = False, epi: int = 0) -> torch.Tensor:
+              tile: int = 0, stem: bool = False, epi: int = 0,
+              fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` [2, Co].
 
     ``stem``: x has 4 channels and w is ``[Co][KH][32]`` (row = KW taps x 4
-    channels, zero padded) - the row-segment gather of the 7x7 stem."""
+    channels, zero padded) - the row-segment gather of the 7x7 stem.
+    ``fp8 = (ex, ew)``: x and w are e4m3 bytes (uint8) holding x*2^-ex and
+    w*2^-ew, ex/ew device int32 scalars; the block-scaled MFMA restores the
+    scales (Ci % 16 == 0)."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
@@ -73,6 +77,10 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
     a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0) | _EPI_FLAGS[epi]
+    if fp8 is not None:
+        assert x.dtype == torch.uint8 and w.dtype == torch.uint8, (x.dtype, w.dtype)
+        a.flags |= 256
+        a.xexp, a.wexp = fp8[0].data_ptr(), fp8[1].data_ptr()
     if bias is not None:
         a.bias = bias.data_ptr()
     if stats is not None:

@@ -1,0 +1,79 @@
+"""fp8 (OCP e4m3) quantisation for the fp8 forward path (csrc/kernels/fp8.hip).
+
+Per-tensor power-of-two scales q = x * 2^-e; the exponents stay on the device
+and the conv kernel feeds them to the block-scaled MFMA as E8M0 scales, so
+neither quantisation nor dequantisation needs a host round trip.
+
+* :class:`WeightQuantizer` -- exact per-step scaling of every conv weight
+  (fp32 master -> e4m3 shadow) in two launches over a descriptor table.
+* :class:`ActScales` -- delayed scaling for activations: slot i's tensor is
+  quantised with the exponent from the previous step's amax, this step's amax
+  is recorded, :meth:`ActScales.step` turns amax into next step's exponents.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence
+
+import torch
+
+from . import _lib
+
+E4M3_MAX = 448.0
+
+
+def quant_act(x: torch.Tensor, exp: torch.Tensor, amax: torch.Tensor = None,
+              out: torch.Tensor = None) -> torch.Tensor:
+    """bf16 tensor -> uint8 e4m3 bytes of x * 2^-exp (exp: device int32 scalar)."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _lib.check(_lib.kernels().imk_quant_fp8(x.data_ptr(), out.data_ptr(), x.numel(), exp.data_ptr(),
+                                            _lib.ptr(amax), _lib.stream_ptr()), "fp8 quant")
+    return out
+
+
+class ActScales:
+    """Device exponents + amax accumulators for ``n`` activation tensors."""
+
+    def __init__(self, n: int, device, margin: int = 0):
+        self.n = n
+        self.exp = torch.zeros(n, dtype=torch.int32, device=device)
+        self.amax = torch.zeros(n, dtype=torch.float32, device=device)
+        self.margin = margin
+
+    def step(self) -> None:
+        _lib.check(_lib.kernels().imk_fp8_update_exp(self.amax.data_ptr(), self.exp.data_ptr(), self.n,
+                                                     self.margin, _lib.stream_ptr()), "fp8 update exp")
+
+
+class WeightQuantizer:
+    """e4m3 shadows of fp32 weights, re-quantised (exact amax) by :meth:`run`."""
+
+    def __init__(self, weights: Sequence[torch.Tensor], device, margin: int = 0):
+        dev = torch.device(device)
+        total = sum((w.numel() + 15) // 16 * 16 for w in weights)
+        self.q = torch.zeros(total, dtype=torch.uint8, device=dev)
+        self.exp = torch.zeros(len(weights), dtype=torch.int32, device=dev)
+        self.amax = torch.zeros(len(weights), dtype=torch.float32, device=dev)
+        self.views: List[torch.Tensor] = []
+        descs = (_lib.QDesc * len(weights))()
+        off = 0
+        max_n4 = 1
+        for i, w in enumerate(weights):
+            assert w.numel() % 4 == 0 and (w.is_contiguous(memory_format=torch.channels_last) or w.is_contiguous())
+            v = self.q[off:off + w.numel()]
+            self.views.append(v)
+            d = descs[i]
+            d.src, d.dst, d.n4 = w.data_ptr(), v.data_ptr(), w.numel() // 4
+            d.exp = self.exp[i:i + 1].data_ptr()
+            d.amax = self.amax[i:i + 1].data_ptr()
+            max_n4 = max(max_n4, w.numel() // 4)
+            off += (w.numel() + 15) // 16 * 16  # 16-B aligned slots
+        self._descs = torch.frombuffer(bytearray(bytes(memoryview(descs))), dtype=torch.uint8).to(dev)
+        self._n, self._max_n4, self.margin = len(weights), max_n4, margin
+
+    def run(self) -> None:
+        self.amax.zero_()
+        _lib.check(_lib.kernels().imk_quant_fp8_weights(self._descs.data_ptr(), self._n, self._max_n4,
+                                                        self.margin, _lib.stream_ptr()), "fp8 weights")

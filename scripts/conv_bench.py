@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
     ap.add_argument("--no-stats", action="store_true", help="forward without the fused BN statistics")
     ap.add_argument("--epi", type=int, default=0, help="0 auto, 1 direct, 2 LDS-staged epilogue")
+    ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3, block-scaled MFMA) forward")
     ap.add_argument("--tiles", default=None, help="comma list of explicit tile ids to time for fwd/dgrad")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
@@ -105,6 +106,14 @@ def main():
             t_m = timeit(lambda: F.conv2d(xc, wc, None, s, p))
             line += f" | {t_m:8.1f}"
             r["miopen_fwd_us"] = t_m
+        if a.fp8 and not stem and Ci % 16 == 0:
+            x8 = x.float().clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+            w8 = w.float().to(torch.float8_e4m3fn).view(torch.uint8)
+            e8 = torch.zeros(2, dtype=torch.int32, device=dev)
+            t8 = timeit(lambda: igemm_fwd(x8, w8, s, p, k, k, stats=stats, fp8=(e8[0:1], e8[1:2])))
+            line += f" | fp8 fwd {t8:8.1f} {flops / t8 / 1e6:6.0f}"
+            r["fp8_fwd_us"] = t8
+            tot["fp8_fwd"] += t8 * cnt
         if a.tiles and not stem:
             for t in (int(v) for v in a.tiles.split(",")):
                 tf = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, tile=t))

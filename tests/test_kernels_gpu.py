@@ -311,3 +311,52 @@ def test_normalize_and_transpose():
     TransposePlan([(a, b, 96, 9, 40), (c, d, 1000, 1, 64)], DEV).run()
     assert torch.equal(b, a.permute(2, 1, 0))
     assert torch.equal(d, c.permute(2, 1, 0))
+
+
+def test_fp8_quant_matches_torch_e4m3():
+    from imagent_amd.ops.fp8 import ActScales, WeightQuantizer, quant_act
+    torch.manual_seed(8)
+    x = bf(torch.randn(4096, device=DEV) * 3)
+    sc = ActScales(1, DEV)
+    sc.exp.fill_(-2)  # q = x * 4
+    q = quant_act(x, sc.exp[0:1], sc.amax[0:1])
+    ref = (x.float() * 4).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q, ref.view(torch.uint8))
+    assert sc.amax.item() == x.float().abs().max().item()
+    sc.step()  # amax ~ 12 -> exponent ceil(log2(12/448)) = -5
+    assert sc.exp.item() == -5 and sc.amax.item() == 0.0
+    w = torch.randn(64, 32, 3, 3, device=DEV).contiguous(memory_format=torch.channels_last)
+    wq = WeightQuantizer([w], DEV)
+    wq.run()
+    e = wq.exp.item()
+    amax = w.abs().max().item()
+    assert amax * 2.0 ** -e <= 448 and amax * 2.0 ** -(e - 1) > 448
+    w_nhwc = w.permute(0, 2, 3, 1).contiguous().flatten()
+    ref = (w_nhwc * 2.0 ** -e).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(wq.views[0], ref)
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("tile", [0, 2, 4, 8])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 2, 0), (3, 16, 11, 64, 3, 1, 1),
+                                   (2, 128, 14, 256, 1, 1, 0), (4, 64, 16, 64, 3, 1, 1), (2, 512, 4, 512, 3, 1, 1)])
+def test_conv_fp8_forward(tile, shape, epi):
+    """Block-scaled fp8 MFMA conv vs fp32 conv of the same dequantised operands."""
+    from imagent_amd.ops.conv import igemm_fwd
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(9)
+    ex, ew = -3, -8
+    x = torch.randn(N, H, H, Ci, device=DEV).abs() * 4  # post-ReLU-like
+    w = torch.randn(Co, k, k, Ci, device=DEV) * 0.05
+    x8 = (x * 2.0 ** -ex).clamp(-448, 448).to(torch.float8_e4m3fn)
+    w8 = (w * 2.0 ** -ew).clamp(-448, 448).to(torch.float8_e4m3fn)
+    xd = x8.float() * 2.0 ** ex
+    wd = w8.float() * 2.0 ** ew
+    yr = F.conv2d(nchw(xd), wd.permute(0, 3, 1, 2), None, s, p)
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    e = torch.tensor([ex, ew], dtype=torch.int32, device=DEV)
+    y = igemm_fwd(x8.view(torch.uint8), w8.view(torch.uint8), s, p, k, k, stats=slab, tile=tile,
+                  fp8=(e[0:1], e[1:2]), epi=epi)
+    assert rel(nchw(y), yr) < 1e-2
+    yb = nchw(y).float()
+    assert rel(slab.sum(0)[0], yb.sum((0, 2, 3))) < 1e-3

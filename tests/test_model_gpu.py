@@ -124,3 +124,77 @@ def test_fused_bn_backward_matches_unfused(arch):
         if e_f > max(0.05, 1.3 * e_u + 0.03):
             bad.append((n, e_u, e_f))
     assert not bad, bad
+
+
+def _fq(t, e):
+    """fake-quantise to OCP e4m3 with scale 2^e (the kernels' saturating rounding)."""
+    return (t * 2.0 ** -e).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** e
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_fp8_forward_training_step(arch, monkeypatch):
+    """--dtype fp8 (e4m3 forward convs, bf16 backward).
+
+    A quantised network is chaotic under ANY perturbation (an fp32 emulation of
+    the same fake-quantisation moves ~20 % when merely run under bf16
+    autocast), so end-to-end parity is not a usable yardstick. Instead, inside
+    the real training forward every fp8 conv is checked exactly: its e4m3
+    operands must be the fake-quantised bf16 activation / fp32 master weight
+    with the tensor's current power-of-two scale, and its output must be the
+    fp32 conv of those operands (up to the bf16 output rounding). End to end:
+    logits near the fp32 oracle, finite gradients, sane delayed scales."""
+    import math
+
+    import imagent_amd.ops.block as blk
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native import bind_native
+    checked = []
+    orig = blk._fwd8
+
+    def checked_fwd8(conv, h, h8, bn):
+        y = orig(conv, h, h8, bn)
+        if h8 is not None:
+            ex, ew = int(h8[1].item()), int(conv.w8_exp.item())
+            w = conv.weight.detach().float()
+            assert ew == math.ceil(math.log2(w.abs().max().item() / 448.0))
+            x8 = h8[0].view(torch.float8_e4m3fn).float() * 2.0 ** ex
+            assert torch.equal(x8, _fq(h.float(), ex))
+            w8 = conv.w8.view(torch.float8_e4m3fn).float().permute(0, 3, 1, 2) * 2.0 ** ew
+            assert torch.equal(w8, _fq(w, ew))
+            ref = F.conv2d(x8.permute(0, 3, 1, 2), w8, None, conv.stride, conv.padding)
+            assert rel(y.permute(0, 3, 1, 2), ref) < 5e-3
+            checked.append(tuple(conv.weight.shape))
+        return y
+
+    monkeypatch.setattr(blk, "_fwd8", checked_fwd8)
+    torch.manual_seed(11)
+    ref = resnet.build(arch, num_classes=1000).to(DEV)
+    model = copy.deepcopy(ref)
+    st = bind_native(model, DEV, fp8=True)
+    with torch.no_grad():
+        for p_ref, p in zip(ref.parameters(), model.parameters()):
+            p_ref.copy_(p.to(torch.bfloat16).float())
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = (torch.rand(16, 64, 64, 4, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    x[..., 3] = 0
+    lab = torch.randint(0, 1000, (16,), device=DEV, generator=g)
+    model.train()
+    ref.train()
+    st.arena.zero_grad()
+    logits = model(x)
+    F.cross_entropy(logits, lab).backward()
+    assert len(checked) == len(model.convs()) - 1  # every conv but the stem ran in fp8
+    l32 = ref(x[..., :3].float().permute(0, 3, 1, 2).contiguous())
+    e_log = rel(logits, l32)
+    print(f"fp8 {arch}: logits rel err vs fp32 {e_log:.3f}")
+    # e4m3 keeps 3 mantissa bits and this random-init net is chaotic (even bf16
+    # autocast moves ResNet-50's logits by 25 % here): a loose sanity bound only
+    assert e_log < 0.75
+    assert all(torch.isfinite(p.grad).all() for p in model.parameters())
+    # the optimizer-step hook re-quantises weights and moves activation scales
+    st.refresh_shadows()
+    assert 0 < int(st.fp8.act.exp.abs().max().item()) < 30
+    checked.clear()
+    st.arena.zero_grad()
+    F.cross_entropy(model(x), lab).backward()
+    assert checked and all(torch.isfinite(p.grad).all() for p in model.parameters())
