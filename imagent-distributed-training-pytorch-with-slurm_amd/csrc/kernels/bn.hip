@@ -43,6 +43,15 @@ __device__ __forceinline__ Vec8 ld8(const bf16_t* p) {
     }
     return r;
 }
+__device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[i] = a[i];
+        o[4 + i] = b[i];
+    }
+}
+
 __device__ __forceinline__ void st8(bf16_t* p, const Vec8& x) {
     u32x4 w;
 #pragma unroll
@@ -76,37 +85,33 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     if (tid >= rpb * cpr) return;  // (host: with y8, every lane is active -- C/8 divides 256)
     const int ch = tid % cpr, c0 = ch * 8;
     float sc[8], sh[8], sc2[8], sh2[8];
+    // per-channel constants by 16-B loads (c0 % 8 == 0, 32-B aligned arrays)
+    auto consts = [&](const float* su, const float* g, const float* b, float* sv, float (&k)[8], float (&o)[8]) {
+        float s0[8], s1[8], gg[8], bb[8];
+        ld8f(su + c0, s0);
+        ld8f(su + C + c0, s1);
+        ld8f(g + c0, gg);
+        ld8f(b + c0, bb);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        float mean, rstd;
-        if (eval) {  // sums holds running_mean / running_var
-            mean = sums[c0 + i];
-            rstd = rsqrtf(sums[C + c0 + i] + eps);
-        } else {
-            mean_rstd(sums, C, c0 + i, inv_cnt, eps, mean, rstd);
-        }
-        sc[i] = rstd * gamma[c0 + i];
-        sh[i] = beta[c0 + i] - mean * sc[i];
-        if (save && blockIdx.x == 0 && tid < cpr) {
-            save[c0 + i] = mean;
-            save[C + c0 + i] = rstd;
-        }
-        if (MODE == 2) {
-            float m2, r2;
-            if (eval) {
-                m2 = sums2[c0 + i];
-                r2 = rsqrtf(sums2[C + c0 + i] + eps);
+        for (int i = 0; i < 8; ++i) {
+            float mean, rstd;
+            if (eval) {  // sums holds running_mean / running_var
+                mean = s0[i];
+                rstd = rsqrtf(s1[i] + eps);
             } else {
-                mean_rstd(sums2, C, c0 + i, inv_cnt, eps, m2, r2);
+                mean = s0[i] * inv_cnt;
+                rstd = rsqrtf(fmaxf(s1[i] * inv_cnt - mean * mean, 0.f) + eps);
             }
-            sc2[i] = r2 * gamma2[c0 + i];
-            sh2[i] = beta2[c0 + i] - m2 * sc2[i];
-            if (save2 && blockIdx.x == 0 && tid < cpr) {
-                save2[c0 + i] = m2;
-                save2[C + c0 + i] = r2;
+            k[i] = rstd * gg[i];
+            o[i] = bb[i] - mean * k[i];
+            if (sv && blockIdx.x == 0 && tid < cpr) {
+                sv[c0 + i] = mean;
+                sv[C + c0 + i] = rstd;
             }
         }
-    }
+    };
+    consts(sums, gamma, beta, save, sc, sh);
+    if (MODE == 2) consts(sums2, gamma2, beta2, save2, sc2, sh2);
     // U rows per thread per iteration, all loads issued before any math: 4x
     // the bytes in flight of a one-row loop (HBM needs ~72 KiB per CU)
     const long step = (long)gridDim.x * rpb;
@@ -131,15 +136,21 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
                 if (MODE == 2) o += fmaf(s[u].v[i], sc2[i], sh2[i]);
                 v[u].v[i] = RELU ? fmaxf(o, 0.f) : o;
             }
-            st8(y + (size_t)r * C + c0, v[u]);
+            u32x4 pw;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pw[i] = pack_bf2(v[u].v[2 * i], v[u].v[2 * i + 1]);
+            *reinterpret_cast<u32x4*>(y + (size_t)r * C + c0) = pw;
             if (y8) {
-                // quantise the bf16-rounded output the bf16 consumers see
+                // quantise the bf16-rounded output the bf16 consumers see (unpacked
+                // from the stored words: one shift / mask per value)
                 float w[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    w[i] = bf2f(f2bf(v[u].v[i]));
-                    m8 = fmaxf(m8, fabsf(w[i]));
+                for (int i = 0; i < 4; ++i) {
+                    w[2 * i] = lo_bf(pw[i]);
+                    w[2 * i + 1] = hi_bf(pw[i]);
                 }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) m8 = fmaxf(m8, fabsf(w[i]));
                 reinterpret_cast<u32x2*>(y8)[((size_t)r * C + c0) / 8] =
                     u32x2{pack4_fp8(w[0] * q8, w[1] * q8, w[2] * q8, w[3] * q8),
                           pack4_fp8(w[4] * q8, w[5] * q8, w[6] * q8, w[7] * q8)};
