@@ -157,9 +157,12 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
             }
         }
     }
-    if (y8) {
+    if (y8) {  // every lane active (host check): block max, one atomic per block into a 32-slot amax row
+        __shared__ float wm[4];
         m8 = wave_max(m8);
-        if ((tid & 63) == 0) atomic_max_pos(amax8, m8);
+        if ((tid & 63) == 0) wm[tid >> 6] = m8;
+        __syncthreads();
+        if (tid == 0) atomic_max_pos(amax8 + (blockIdx.x & 31), fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
     }
 }
 
@@ -391,7 +394,8 @@ int grid_for(long R, int C) {
 }  // namespace
 
 // mode: 0 plain, 1 + identity residual (x2), 2 + second BN branch (x2, sums2, gamma2, beta2)
-// y8 (optional): e4m3 copy of y quantised with 2^-exp8[0]; amax8 receives max |y|
+// y8 (optional): e4m3 copy of y quantised with 2^-exp8[0]; amax8 ([32] slots,
+// folded by imk_fp8_update_exp) receives max |y|
 IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, const float* beta,
                           const void* x2, const float* sums2, const float* gamma2, const float* beta2,
                           void* y, float* save, float* save2, long R, int C, int mode, int relu,

@@ -16,6 +16,8 @@
 
 namespace {
 
+constexpr int AMAX_SLOTS = 32;  // per-tensor amax slots (atomic max spread by block id)
+
 // exponent e with amax * 2^-e <= 448 (>= 2^-margin headroom), clamped
 __device__ __forceinline__ int exp_for(float amax, int margin) {
     if (!(amax > 0.f)) return 0;
@@ -44,16 +46,23 @@ __global__ __launch_bounds__(256) void quant_act_kernel(const bf16_t* __restrict
         o[1] = pack4_fp8(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
         reinterpret_cast<u32x2*>(y)[i] = o;
     }
+    __shared__ float wm[4];
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0 && amax) atomic_max_pos(amax, m);
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0 && amax)
+        atomic_max_pos(amax + (blockIdx.x & (AMAX_SLOTS - 1)), fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
 }
 
+// one wave per tensor: fold its AMAX_SLOTS slots, exponent for the next step, clear
 __global__ void update_exp_kernel(float* __restrict__ amax, int* __restrict__ e, int n, int margin) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float a = amax[i];
-    if (a > 0.f) e[i] = exp_for(a, margin);  // no observation: keep the exponent
-    amax[i] = 0.f;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (t >= n) return;
+    float* row = amax + (size_t)t * AMAX_SLOTS;
+    float a = lane < AMAX_SLOTS ? row[lane] : 0.f;
+    a = wave_max(a);
+    if (lane < AMAX_SLOTS) row[lane] = 0.f;
+    if (lane == 0 && a > 0.f) e[t] = exp_for(a, margin);  // no observation: keep the exponent
 }
 
 struct QDesc {
@@ -91,7 +100,7 @@ __global__ __launch_bounds__(256) void weight_quant_kernel(const QDesc* __restri
 }  // namespace
 
 // x: bf16 [n] (n % 8 == 0, 16-B aligned) -> y: e4m3 [n]; exp_in: device int;
-// amax (device float, may be null) receives max |x| (atomic max)
+// amax (device float[32] slots, may be null) receives max |x|
 IMK_EXPORT int imk_quant_fp8(const void* x, void* y, long n, const int* exp_in, float* amax, void* stream) {
     if (n % 8) return -100;
     const long n8 = n / 8;
@@ -104,10 +113,10 @@ IMK_EXPORT int imk_quant_fp8(const void* x, void* y, long n, const int* exp_in, 
     return 0;
 }
 
-// e[i] = exponent for amax[i] (delayed scaling for the next step); amax[i] = 0
+// e[i] = exponent for max(amax[i][0..31]) (delayed scaling, next step); amax rows cleared
 IMK_EXPORT int imk_fp8_update_exp(float* amax, int* e, int n, int margin, void* stream) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(update_exp_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, amax, e, n,
+    hipLaunchKernelGGL(update_exp_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, amax, e, n,
                        margin);
     IMK_CHECK_LAUNCH();
     return 0;

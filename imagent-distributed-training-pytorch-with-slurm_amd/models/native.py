@@ -197,7 +197,7 @@ class Fp8State:
         if like.shape[-1] % 16 or 256 % (like.shape[-1] // 8):
             return None
         return (torch.empty(like.shape, dtype=torch.uint8, device=like.device), self.act.exp[slot:slot + 1],
-                self.act.amax[slot:slot + 1])
+                self.act.amax[slot])
 
     def register(self, y: torch.Tensor, q8) -> None:
         if q8 is not None:

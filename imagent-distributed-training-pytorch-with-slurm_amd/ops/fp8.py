@@ -21,11 +21,13 @@ import torch
 from . import _lib
 
 E4M3_MAX = 448.0
+AMAX_SLOTS = 32  # fp8.hip / bn.hip: per-tensor amax row, folded by imk_fp8_update_exp
 
 
 def quant_act(x: torch.Tensor, exp: torch.Tensor, amax: torch.Tensor = None,
               out: torch.Tensor = None) -> torch.Tensor:
-    """bf16 tensor -> uint8 e4m3 bytes of x * 2^-exp (exp: device int32 scalar)."""
+    """bf16 tensor -> uint8 e4m3 bytes of x * 2^-exp (exp: device int32 scalar);
+    ``amax``: the tensor's [AMAX_SLOTS] row of :class:`ActScales`."""
     if out is None:
         out = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     _lib.check(_lib.kernels().imk_quant_fp8(x.data_ptr(), out.data_ptr(), x.numel(), exp.data_ptr(),
@@ -39,7 +41,7 @@ class ActScales:
     def __init__(self, n: int, device, margin: int = 0):
         self.n = n
         self.exp = torch.zeros(n, dtype=torch.int32, device=device)
-        self.amax = torch.zeros(n, dtype=torch.float32, device=device)
+        self.amax = torch.zeros(n, AMAX_SLOTS, dtype=torch.float32, device=device)  # spread atomics
         self.margin = margin
 
     def step(self) -> None:
