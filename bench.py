@@ -53,6 +53,8 @@ def main(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
+                    help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward")
     a = ap.parse_args(argv)
@@ -88,8 +90,13 @@ def main(argv=None):
     comm = make_communicator(ctx, "rccl" if a.kernels == "hip" else "torch" if ctx.world_size > 1 else "local")
     ddp = DataParallel(model, arena, comm, bucket_cap_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                        rebuild_buckets=False)
-    opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4,
-                  after_step=native.refresh_shadows if native else None)
+    after = native.refresh_shadows if native else None
+    if a.optimizer == "lars":
+        from imagent_amd.train.optim import FlatLARS
+        opt = FlatLARS(arena, lr=0.1 * a.batch_size * a.gpus / 256, momentum=0.9, weight_decay=5e-5, eta=1e-3,
+                       after_step=after)
+    else:
+        opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=after)
     metrics = DeviceMetrics(dev)
     runner = StepRunner(ddp, opt, metrics, a.kernels, 0.0,
                         torch.bfloat16 if a.kernels == "torch" else None)
@@ -142,7 +149,8 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{a.gpus}",
                 "kernels": a.kernels,
-                "optimizer": "sgd(momentum=0.9, wd=1e-4)",
+                "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
+                             "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
                 "grad_allreduce": "fp32 bucketed RCCL avg, side stream",
                 "bucket_mb": a.bucket_mb,
                 "mean_train_loss": round(loss, 4),

@@ -33,8 +33,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet34", "resnet50", "resnet101",
                                                            "resnet152"])
     p.add_argument("--image-size", type=int, default=448)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                   help="compute dtype (HIP kernels: bf16 with fp32 masters/accumulation)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
+                   help="compute dtype. HIP kernels: bf16 (fp32 masters/accumulation), or fp8 = e4m3 "
+                        "forward convs on the block-scaled MFMA with bf16 backward; fp32 = torch oracle path")
     p.add_argument("--data", default="imagenet", choices=["imagenet", "synthetic"])
     p.add_argument("--data-root", default=None, help="default: <cwd>/../data/imagenet (imagenet.py:287)")
     p.add_argument("--workers", type=int, default=10)
@@ -44,7 +45,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--flip", action="store_true", help="random horizontal flip (reference: none)")
     # --- optimisation ---
     p.add_argument("--optimizer", default="sgd",
-                   choices=["sgd", "adam", "adamw", "adagrad", "rmsprop", "adadelta", "asgd", "nadam"])
+                   choices=["sgd", "lars", "adam", "adamw", "adagrad", "rmsprop", "adadelta", "asgd", "nadam"])
+    p.add_argument("--lars-eta", type=float, default=1e-3, help="LARS trust coefficient")
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--wd", "--weight-decay", dest="wd", type=float, default=1e-4)
     p.add_argument("--nesterov", action="store_true")

@@ -90,6 +90,12 @@ class IGemmArgs(C.Structure):
     ]
 
 
+class LarsDesc(C.Structure):
+    """optim.hip LarsDesc: one parameter tensor of the flat arena."""
+    _fields_ = [("p", C.c_void_p), ("g", C.c_void_p), ("buf", C.c_void_p), ("shadow", C.c_void_p),
+                ("n", C.c_long), ("adapt", C.c_int), ("pad", C.c_int)]
+
+
 class QDesc(C.Structure):
     """fp8.hip QDesc: one weight tensor of the per-step e4m3 quantisation."""
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("n4", C.c_long), ("exp", C.c_void_p),
@@ -150,7 +156,8 @@ def _declare(name: str, lib) -> None:
             "imk_quant_fp8": [vp, vp, i64, vp, vp, vp],
             "imk_fp8_update_exp": [vp, vp, i32, i32, vp],
             "imk_quant_fp8_weights": [vp, i32, i64, i32, vp],
-            "imk_qdesc_size": [],
+            "imk_qdesc_size": [], "imk_lars_desc_size": [],
+            "imk_lars_step": [vp, i32, i64, vp, f32, f32, f32, f32, f32, i32, vp],
         }
         for fn, args in sigs.items():
             f = getattr(lib, fn)
@@ -159,7 +166,7 @@ def _declare(name: str, lib) -> None:
         # ABI guard: the ctypes mirrors must match the compiled structs
         for fn, st in [("imk_igemm_args_size", IGemmArgs), ("imk_wgrad_args_size", WgradArgs),
                        ("imk_bn_rundesc_size", RunDesc), ("imk_tdesc_size", TDesc),
-                       ("imk_qdesc_size", QDesc)]:
+                       ("imk_qdesc_size", QDesc), ("imk_lars_desc_size", LarsDesc)]:
             n = getattr(lib, fn)()
             if n != C.sizeof(st):
                 raise RuntimeError(f"{fn}: native {n} B != ctypes {C.sizeof(st)} B - rebuild")

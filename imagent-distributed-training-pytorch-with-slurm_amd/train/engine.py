@@ -145,7 +145,9 @@ class Trainer:
         _master_print(self.is_master, "Training samples: {} images ".format(self.n_train))
         _master_print(self.is_master, "Test samples: {} images ".format(self.n_val))
         _master_print(self.is_master, "number of classes: {}".format(self.num_classes))
-        self.dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype]
+        self.dtype = {"bf16": torch.bfloat16, "fp8": torch.bfloat16, "fp32": torch.float32}[a.dtype]
+        if a.dtype == "fp8" and self.kernels != "hip":
+            raise SystemExit("--dtype fp8 needs the HIP kernels (--kernels hip on a MI355X)")
         self.transform_train = InputTransform(self.kernels, size, cpad=resnet.ResNet.STEM_CPAD,
                                               flip=a.flip,
                                               dtype=torch.float32)
@@ -177,7 +179,7 @@ class Trainer:
         self.native = None
         if self.kernels == "hip":
             from ..models.native import bind_native
-            self.native = bind_native(model, self.device, order)
+            self.native = bind_native(model, self.device, order, fp8=a.dtype == "fp8")
             arena = self.native.arena
         else:
             model.to(self.device)
@@ -192,7 +194,7 @@ class Trainer:
         full = (lambda: self.native.refresh_shadows(full=True)) if self.native else None
         self.opt = build_optimizer(a.optimizer, arena, a.lr, a.momentum, a.wd, a.nesterov,
                                    after_step=after, full_refresh=full,
-                                   schedule_decay=a.schedule_decay)
+                                   schedule_decay=a.schedule_decay, lars_eta=a.lars_eta)
         self.metrics = DeviceMetrics(self.device)
         from ..utils.profiling import StepTimer
         self.timer = StepTimer(enabled=self.device.type == "cuda")

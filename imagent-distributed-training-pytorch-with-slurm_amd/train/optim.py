@@ -14,6 +14,7 @@ reference, quirk Q5).
   views (updates land in the arena) followed by a shadow refresh.
   ``nadam`` maps Keras' ``schedule_decay`` to torch's ``momentum_decay`` (the
   same psi in mu_t = beta1 * (1 - 0.5 * 0.96 ** (t * psi))).
+* :class:`FlatLARS` - LARS for the large-batch (8192) configuration.
 * ``fr`` is deliberately absent: the reference never defines it.
 """
 
@@ -106,6 +107,85 @@ class FlatSGD:
             self.buf = None
 
 
+class FlatLARS(FlatSGD):
+    """LARS (You, Gitman, Ginsburg 2017) for large-batch runs (the fp8 8192
+    config): per tensor trust = eta * ||w|| / (||g|| + wd * ||w||),
+    v = mu * v + lr * trust * (g + wd * w), w -= v. One-dimensional tensors
+    (BatchNorm affine, biases) are neither adapted nor decayed. On the GPU it
+    is two launches over a per-tensor descriptor table (csrc/kernels/optim.hip);
+    on CPU the same math per tensor."""
+
+    def __init__(self, arena: ParamArena, lr: float, momentum: float = 0.9, weight_decay: float = 1e-4,
+                 eta: float = 1e-3, native: Optional[bool] = None, after_step: Optional[Callable[[], None]] = None):
+        super().__init__(arena, lr, momentum, 0.0, weight_decay, False, native, after_step)
+        self.param_groups[0]["eta"] = eta
+        self._descs = None
+
+    def _build_descs(self):
+        import ctypes as C
+
+        from ..ops import _lib
+        ar = self.arena
+        T = len(ar.params)
+        d = (_lib.LarsDesc * T)()
+        for i in range(T):
+            o, n = ar.offsets[i], ar.numels[i]
+            d[i].p = ar.P[o:o + n].data_ptr()
+            d[i].g = ar.G[o:o + n].data_ptr()
+            d[i].buf = self.buf[o:o + n].data_ptr()
+            d[i].shadow = ar.S[o:o + n].data_ptr() if ar.S is not None else None
+            d[i].n = n
+            d[i].adapt = 1 if len(ar.shapes[i]) > 1 else 0
+        self._descs = torch.frombuffer(bytearray(bytes(memoryview(d))), dtype=torch.uint8).to(ar.P.device)
+        self._norms = torch.zeros(2 * T, dtype=torch.float32, device=ar.P.device)
+        self._key = (ar.P.data_ptr(), ar.G.data_ptr(), self.buf.data_ptr())
+        self._max_n = max(ar.numels)
+        del C
+
+    @torch.no_grad()
+    def step(self) -> None:
+        g = self.param_groups[0]
+        lr, mu, wd, eta = g["lr"], g["momentum"], g["weight_decay"], g["eta"]
+        ar = self.arena
+        first = self.buf is None
+        if first:
+            self.buf = torch.zeros_like(ar.P)
+        if self.native:
+            from ..ops import _lib
+            if self._descs is None or self._key != (ar.P.data_ptr(), ar.G.data_ptr(), self.buf.data_ptr()):
+                self._build_descs()  # (re)built after a bucket re-layout moved the arenas
+            _lib.check(_lib.kernels().imk_lars_step(self._descs.data_ptr(), len(ar.params), self._max_n,
+                                                    self._norms.data_ptr(), lr, mu, wd, eta, self.grad_scale,
+                                                    1 if first else 0, _lib.stream_ptr()), "lars step")
+        else:
+            for i in range(len(ar.params)):
+                w, gr, v = ar.flat_slice(ar.P, i), ar.flat_slice(ar.G, i) * self.grad_scale, \
+                    ar.flat_slice(self.buf, i)
+                adapt = len(ar.shapes[i]) > 1
+                trust, wdt = 1.0, 0.0
+                if adapt:
+                    wdt = wd
+                    wn, gn = w.norm().item(), gr.norm().item()
+                    if wn > 0 and gn > 0:
+                        trust = eta * wn / (gn + wd * wn)
+                d = gr + wdt * w
+                if first:
+                    v.copy_(lr * trust * d)
+                else:
+                    v.mul_(mu).add_(d, alpha=lr * trust)
+                w.sub_(v)
+            if ar.S is not None:
+                ar.S.copy_(ar.P)
+        self.steps += 1
+        if self.after_step is not None:
+            self.after_step()
+
+    def state_dict(self) -> Dict:
+        sd = super().state_dict()
+        sd["kind"] = "lars"
+        return sd
+
+
 class TorchOptimizer:
     """A stock torch.optim optimizer over the arena views + shadow refresh."""
 
@@ -152,6 +232,8 @@ def build_optimizer(name: str, arena: ParamArena, lr: float, momentum: float = 0
     if name == "sgd":
         return FlatSGD(arena, lr, momentum, kw.get("dampening", 0.0), weight_decay, nesterov,
                        after_step=after_step)
+    if name == "lars":
+        return FlatLARS(arena, lr, momentum, weight_decay, eta=kw.get("lars_eta", 1e-3), after_step=after_step)
     if name == "adagrad":
         o = torch.optim.Adagrad(params, lr=lr, lr_decay=0, weight_decay=weight_decay,
                                 initial_accumulator_value=0, eps=1e-10)

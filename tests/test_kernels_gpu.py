@@ -360,3 +360,27 @@ def test_conv_fp8_forward(tile, shape, epi):
     assert rel(nchw(y), yr) < 1e-2
     yb = nchw(y).float()
     assert rel(slab.sum(0)[0], yb.sum((0, 2, 3))) < 1e-3
+
+
+def test_lars_native_matches_cpu_math():
+    import torch.nn as nn
+
+    from imagent_amd.models.arena import ParamArena
+    from imagent_amd.train.optim import FlatLARS
+    torch.manual_seed(3)
+    nets = [nn.Sequential(nn.Conv2d(16, 32, 3), nn.BatchNorm2d(32), nn.Flatten(), nn.Linear(32, 10))
+            for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    ar_g = ParamArena(list(nets[0].named_parameters()), torch.device(DEV), with_shadow=True)
+    ar_c = ParamArena(list(nets[1].named_parameters()), torch.device("cpu"))
+    og = FlatLARS(ar_g, lr=2.0, momentum=0.9, weight_decay=5e-5, eta=1e-3)
+    oc = FlatLARS(ar_c, lr=2.0, momentum=0.9, weight_decay=5e-5, eta=1e-3, native=False)
+    assert og.native
+    for _ in range(3):
+        g = torch.randn(ar_c.total)
+        ar_c.G.copy_(g)
+        ar_g.G.copy_(g.to(DEV))
+        og.step()
+        oc.step()
+    assert torch.allclose(ar_g.P.cpu(), ar_c.P, rtol=1e-4, atol=1e-6)
+    assert torch.equal(ar_g.S.cpu(), ar_g.P.cpu().to(torch.bfloat16))

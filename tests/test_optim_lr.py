@@ -87,3 +87,31 @@ def test_meters_and_accuracy():
     dm.update_from_logits(out, t, torch.tensor(1.5))
     loss, t1, t5, n = dm.reduced()
     assert (loss, t1, t5, n) == (1.5, 50.0, 100.0, 2.0)
+
+
+def test_lars_matches_reference_math():
+    """FlatLARS (CPU path) vs a direct per-parameter LARS reference, 3 steps."""
+    import torch.nn as nn
+
+    from imagent_amd.models.arena import ParamArena
+    from imagent_amd.train.optim import FlatLARS
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Conv2d(3, 8, 3), nn.BatchNorm2d(8))
+    ref = [p.detach().clone() for p in net.parameters()]
+    ar = ParamArena(list(net.named_parameters()), torch.device("cpu"))
+    opt = FlatLARS(ar, lr=0.5, momentum=0.9, weight_decay=1e-4, eta=1e-3, native=False)
+    vel = [torch.zeros_like(p) for p in ref]
+    for step in range(3):
+        grads = [torch.randn_like(p) for p in ref]
+        for p, g in zip(net.parameters(), grads):
+            p.grad.copy_(g)
+        opt.step()
+        for i, (w, g) in enumerate(zip(ref, grads)):
+            adapt = w.dim() > 1
+            wd = 1e-4 if adapt else 0.0
+            trust = 1e-3 * w.norm() / (g.norm() + 1e-4 * w.norm()) if adapt else 1.0
+            d = g + wd * w
+            vel[i] = 0.5 * trust * d if step == 0 else 0.9 * vel[i] + 0.5 * trust * d
+            w -= vel[i]
+    for p, w in zip(net.parameters(), ref):
+        assert torch.allclose(p.detach(), w, rtol=1e-5, atol=1e-6)
