@@ -53,6 +53,7 @@ def main(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
+    ap.add_argument("--wgrad-overlap", type=int, default=1, help="0: weight gradients on the main stream")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
                     help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
@@ -82,7 +83,8 @@ def main(argv=None):
     native = None
     if a.kernels == "hip":
         from imagent_amd.models.native import bind_native
-        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8")
+        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8",
+                             wgrad_overlap=bool(a.wgrad_overlap))
         arena = native.arena
     else:
         model.to(dev)

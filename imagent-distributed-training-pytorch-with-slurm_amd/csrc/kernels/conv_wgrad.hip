@@ -33,7 +33,7 @@ struct WgradArgs {
     int KH, KW, stride, pad;
     int m_per_split;   // multiple of BR
     uint32_t mg_ohw, sh_ohw, mg_ow, sh_ow;  // magic division by OH*OW and OW
-    int stem;          // 1: C == 4 row-segment gather, dW is [Co][KH][32]
+    int stem;          // bit 0: C == 4 row-segment gather, dW is [Co][KH][32]
 };
 
 namespace {
@@ -248,12 +248,14 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     const WgradArgs& a = *args;
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (a.stem) {
+    if (a.stem & 1) {
         if (a.Ci != 4 || a.KW > 8 || a.Co % 8) return -102;
         return launch<64, 128, 1, true>(a, splits, st);
     }
     if (a.Ci % 8 || a.Co % 8) return -100;
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
+    // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
+    // 2 % slower than this register-staged loop on every R50 shape: not kept)
     // (launch<256, 256, 2, false, 8> -- one 8-wave block per CU -- measured 23 %
     // slower in total: this register-staged loop needs two blocks per CU)
     return launch<128, 128, 2, false>(a, splits, st);

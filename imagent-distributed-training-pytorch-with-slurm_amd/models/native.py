@@ -32,7 +32,7 @@ def stem_view(t: torch.Tensor, kw: int) -> torch.Tensor:
 
 class NativeState:
     def __init__(self, model: ResNet, device: torch.device, order: Optional[Sequence[int]] = None,
-                 bnb_fusion: bool = True, fp8: bool = False):
+                 bnb_fusion: bool = True, fp8: bool = False, wgrad_overlap: bool = True):
         self.device = torch.device(device)
         named = list(model.named_parameters())
         self.arena = ParamArena(named, self.device, order=order, with_shadow=True)
@@ -51,6 +51,9 @@ class NativeState:
             b._bnb_done = False
         self._bind_shadows()
         self._bind_workspace()
+        # weight-gradient kernels on a second HIP stream (ops/streams.py)
+        from ..ops import streams
+        streams.set_wgrad_overlap(wgrad_overlap)
         self.fp8 = None
         if fp8:
             self.fp8 = Fp8State(self)
@@ -208,9 +211,9 @@ class Fp8State:
 
 
 def bind_native(model: ResNet, device, order: Optional[Sequence[int]] = None,
-                bnb_fusion: bool = True, fp8: bool = False) -> NativeState:
+                bnb_fusion: bool = True, fp8: bool = False, wgrad_overlap: bool = True) -> NativeState:
     model.to(device)
-    st = NativeState(model, device, order, bnb_fusion=bnb_fusion, fp8=fp8)
+    st = NativeState(model, device, order, bnb_fusion=bnb_fusion, fp8=fp8, wgrad_overlap=wgrad_overlap)
     model.native = st
     model.backend = "hip"
     st.refresh_shadows(full=True)

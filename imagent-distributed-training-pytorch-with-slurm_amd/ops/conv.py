@@ -17,7 +17,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, streams
 from .grad_sink import notify_ready
 
 
@@ -225,7 +225,21 @@ class ConvFn(torch.autograd.Function):
 
 def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
     """Accumulate a Conv2d module's weight gradient into its arena slot and
-    signal the bucketed reducer."""
+    signal the bucketed reducer (on the wgrad side stream when enabled,
+    ``ops/streams.py``)."""
+    side = streams.side_stream(dy.device) if dy.is_cuda else None
+    if side is None:
+        _conv_wgrad(mod, dy, x)
+        return
+    side.wait_stream(torch.cuda.current_stream(dy.device))
+    with torch.cuda.stream(side):
+        _conv_wgrad(mod, dy, x)
+    dy.record_stream(side)
+    x.record_stream(side)
+    streams.ensure_join_after_backward()
+
+
+def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
     gp = getattr(mod, "grad_pad", None)
     if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
         gp.zero_()

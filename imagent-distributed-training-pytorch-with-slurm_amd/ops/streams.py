@@ -1,0 +1,79 @@
+"""Side stream for weight-gradient kernels (backward overlap).
+
+In backward, a conv's dgrad (feeds the next layer's backward: critical path)
+and its wgrad (feeds only the gradient arena and the all-reduce) both consume
+the same upstream gradient and are independent. Queuing every wgrad on a
+second HIP stream lets it fill the CUs the critical-path kernels leave idle
+(wave-quantisation tails, small late-stage grids) instead of serialising.
+
+Dependencies that make this safe:
+* the side stream waits for the main stream before each wgrad (its inputs);
+* tensors read on the side stream are ``record_stream``-ed so the caching
+  allocator does not recycle them early;
+* the data-parallel reducer makes each bucket's all-reduce wait for the side
+  stream as well as the main one (``parallel/ddp.py``), and the end of
+  backward joins the side stream into the main one (the optimizer reads the
+  gradient arena).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+_enabled = False
+_streams: Dict[int, torch.cuda.Stream] = {}
+
+
+def set_wgrad_overlap(on: bool) -> None:
+    global _enabled
+    _enabled = bool(on)
+
+
+def side_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.Stream]:
+    """The wgrad stream of ``device`` (None when the overlap is off or on CPU)."""
+    if not _enabled or not torch.cuda.is_available():
+        return None
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    s = _streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _streams[idx] = s
+    return s
+
+
+def active_side_stream() -> Optional[torch.cuda.Stream]:
+    """The side stream if one has been used on the current device."""
+    if not _enabled or not torch.cuda.is_available():
+        return None
+    return _streams.get(torch.cuda.current_device())
+
+
+def join_side_into_current() -> None:
+    s = active_side_stream()
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
+_join_queued = False
+
+
+def _join_cb() -> None:
+    global _join_queued
+    _join_queued = False
+    join_side_into_current()
+
+
+def ensure_join_after_backward() -> None:
+    """Queue (once per backward pass) a join of the side stream into the main
+    stream, so whoever reads ``.grad`` after ``backward()`` sees finished
+    gradients even without the data-parallel reducer."""
+    global _join_queued
+    if _join_queued:
+        return
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(_join_cb)
+        _join_queued = True
+    except RuntimeError:  # not inside a backward pass: join right away
+        join_side_into_current()

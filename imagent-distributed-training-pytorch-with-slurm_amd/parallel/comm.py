@@ -52,6 +52,11 @@ class Communicator:
     def close(self) -> None:
         pass
 
+    def depend_on(self, stream) -> None:
+        """Collectives issued after this call also wait for ``stream``."""
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().wait_stream(stream)
+
 
 class LocalCommunicator(Communicator):
     name = "local"
@@ -168,6 +173,10 @@ class RcclCommunicator(Communicator):
         out.record_stream(self.stream)
         self.join()
         return out
+
+    def depend_on(self, stream) -> None:
+        if self.world_size > 1:  # the comm stream waits; the compute stream keeps going
+            self._chk(self.L.imc_stream_join_from(self.h, stream.cuda_stream), "join_from")
 
     def join(self):
         self._chk(self.L.imc_stream_join_into(self.h, self._cur()), "join")

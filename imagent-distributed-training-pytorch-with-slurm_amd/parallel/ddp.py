@@ -39,7 +39,7 @@ import torch
 import torch.nn as nn
 
 from ..models.arena import ParamArena
-from ..ops import _lib
+from ..ops import _lib, streams
 from .comm import Communicator, LocalCommunicator
 
 MB = 1024 * 1024
@@ -271,6 +271,11 @@ class DataParallel(nn.Module):
 
     def _launch(self, b: int):
         lo, hi, _ = self.buckets[b]
+        side = streams.active_side_stream()
+        if side is not None:
+            # bucket members may have been produced on the wgrad side stream:
+            # the all-reduce waits for it too (main stream not blocked)
+            self.comm.depend_on(side)
         self.comm.allreduce_(self.arena.G[lo:hi], "avg")
 
     def _finalize_backward(self):
@@ -286,6 +291,7 @@ class DataParallel(nn.Module):
             # unused parameters contribute zeros: launch the remaining buckets in order
             for b in range(len(self.buckets) - missing, len(self.buckets)):
                 self._launch(b)
+        streams.join_side_into_current()  # the optimizer reads the gradient arena
         self.comm.join()
         self.iteration += 1
         self.last_order = order

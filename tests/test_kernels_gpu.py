@@ -128,6 +128,24 @@ def test_conv_lds_epilogue(tile, shape):
     assert rel(acc.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
+@pytest.mark.parametrize("splits", [0, 3])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 512, 1, 2, 0),
+                                   (2, 128, 7, 256, 3, 1, 1), (5, 96, 13, 136, 1, 1, 0)])
+def test_wgrad_variants(shape, splits):
+    """Weight gradient incl. ragged Co / K tails and explicit split-K."""
+    from imagent_amd.ops.conv import igemm_wgrad
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(6)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = torch.randn(Co, Ci, k, k, device=DEV).requires_grad_(True)
+    yr = F.conv2d(x.float(), w, None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    dw = torch.zeros(Co, k, k, Ci, device=DEV)
+    igemm_wgrad(nhwc(g), nhwc(x), dw, s, p, k, k, splits=splits)
+    assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3
+
+
 def test_stem_row_segment_conv():
     """7x7/s2 stem: 4-channel NHWC input, [Co][KH][32] weight rows (fwd + wgrad)."""
     from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
