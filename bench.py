@@ -54,6 +54,8 @@ def main(argv=None):
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
     ap.add_argument("--wgrad-overlap", type=int, default=1, help="0: weight gradients on the main stream")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture the whole step in a HIP graph and replay it (1 GPU; launch-bound small batches)")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
                     help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
@@ -109,9 +111,18 @@ def main(argv=None):
     tf = InputTransform(a.kernels, (a.image_size, a.image_size), cpad=resnet.ResNet.STEM_CPAD)
     model.train()
 
+    def one(u8, y):
+        runner.train_step([(tf(u8), y)])
+
+    if a.graph:
+        if ctx.world_size > 1:
+            raise SystemExit("--graph is validated for one GPU only")
+        from imagent_amd.train.engine import GraphedStep
+        one = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr)
+
     def steps(n):
         for u8, y in src.batches(n):
-            runner.train_step([(tf(u8), y)])
+            one(u8, y)
 
     steps(a.warmup)
     ctx.barrier()
@@ -151,6 +162,7 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{a.gpus}",
                 "kernels": a.kernels,
+                "hip_graph": bool(a.graph),
                 "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
                              "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
                 "grad_allreduce": "fp32 bucketed RCCL avg, side stream",

@@ -69,6 +69,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--broadcast-buffers", default="eval", choices=["eval", "always", "never"])
     p.add_argument("--no-rebuild-buckets", dest="rebuild_buckets", action="store_false")
     p.add_argument("--pg-timeout", type=float, default=1800.0)
+    p.add_argument("--hip-graph", action="store_true",
+                   help="capture each training step in a HIP graph and replay it (1 GPU, step LR schedule)")
     p.add_argument("--step-timeout", type=float, default=0.0,
                    help="dump all stacks if one training step exceeds this many seconds (hang detector)")
     p.add_argument("--check-consistency", type=int, default=0,

@@ -84,6 +84,54 @@ class StepRunner:
         self.loss(self.forward(x), y)
 
 
+class GraphedStep:
+    """A whole training step captured once into a HIP graph and replayed.
+
+    ``fn(*inputs)`` (input normalisation -> forward -> loss -> backward with
+    the bucketed all-reduce -> optimizer) runs eagerly for ``warmup`` calls
+    (kernel-variant caches, momentum buffers, bucket rebuild, BN descriptor
+    upload all settle), is then captured with ``torch.cuda.graph`` on static
+    copies of its inputs, and every later call copies the new inputs in and
+    replays: ~400 kernel launches become one graph launch, which is what
+    bounds small per-GPU batches. The capture is keyed on the input shapes and
+    on ``key_fn()`` (e.g. the learning rate, a kernel argument): a change
+    re-captures. Host-side counters are not advanced by replays.
+    """
+
+    def __init__(self, fn, warmup: int = 3, key_fn=None):
+        self.fn, self.warmup, self.key_fn = fn, warmup, key_fn
+        self.graph = None
+        self.static = None
+        self.key = None
+        self.eager_calls = 0
+        self.replays = 0
+
+    def __call__(self, *inputs):
+        key = (tuple((t.shape, t.dtype) for t in inputs), self.key_fn() if self.key_fn else None)
+        if self.graph is not None and key == self.key:
+            for dst, src in zip(self.static, inputs):
+                dst.copy_(src, non_blocking=True)
+            self.graph.replay()
+            self.replays += 1
+            return
+        if self.eager_calls < self.warmup or self.graph is not None:
+            # warm-up, or a key change: one eager step under the new key first
+            self.fn(*inputs)
+            self.eager_calls += 1
+            if self.graph is not None:
+                self.graph = None
+                self.eager_calls = self.warmup
+            return
+        self.static = [t.clone() for t in inputs]
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.fn(*self.static)
+        self.graph, self.key = g, key
+        g.replay()  # the capture only recorded: run this step's work
+        self.replays += 1
+
+
 class _null:
     def __enter__(self):
         return self
@@ -203,6 +251,12 @@ class Trainer:
         if self.kernels == "torch" and self.device.type == "cuda" and a.dtype == "bf16":
             ac = torch.bfloat16
         self.step = StepRunner(self.ddp, self.opt, self.metrics, self.kernels, a.label_smoothing, ac)
+        self._graph_step = None
+        if getattr(a, "hip_graph", False):
+            if self.device.type != "cuda" or self.ctx.world_size > 1:
+                raise SystemExit("--hip-graph: single-GPU runs only (the RCCL path is not captured)")
+            self._graph_step = GraphedStep(lambda x, y: self.step.train_step([(x, y)]), warmup=3,
+                                           key_fn=lambda: self.opt.param_groups[0]["lr"])
         self.start_epoch = 0
         self.best = dict(top1=0.0, top5=0.0, epoch_top1=0, epoch_top5=0, time=0.0)
         if a.resume and os.path.exists(a.resume):
@@ -238,7 +292,16 @@ class Trainer:
         micro = []
         it = 0
         max_steps = a.max_steps if a.max_steps > 0 else math.inf
-        for x, y in train_loader:
+        data_wait = 0.0  # host time blocked on the input pipeline (quirk Q3: measured AND reported)
+        loader_it = iter(train_loader)
+        graph = self._graph_step if (accum == 1 and not per_iter) else None
+        while True:
+            tw = time.perf_counter()
+            try:
+                x, y = next(loader_it)
+            except StopIteration:
+                break
+            data_wait += time.perf_counter() - tw
             micro.append((x, y))
             if len(micro) < accum:
                 continue
@@ -247,7 +310,10 @@ class Trainer:
             if a.step_timeout > 0:   # hang detector: dump every thread's stack if a step stalls
                 faulthandler.dump_traceback_later(a.step_timeout, exit=False)
             self.timer.mark()
-            self.step.train_step(micro)
+            if graph is not None:
+                graph(*micro[0])
+            else:
+                self.step.train_step(micro)
             if a.step_timeout > 0:
                 faulthandler.cancel_dump_traceback_later()
             if a.check_consistency and (it + 1) % a.check_consistency == 0:
@@ -276,6 +342,7 @@ class Trainer:
         loss, t1, t5, n = self.metrics.reduced(self.comm)
         self.last_train_images = n
         self.last_lr = lr
+        self.last_data_wait = data_wait
         self.last_step_pct = self.timer.percentiles()
         self.timer.events.clear()
         return loss, t1, t5, dt
@@ -327,6 +394,7 @@ class Trainer:
                 print(f"\tTrain time: {t_train} seconds; Test time:{t_val} seconds")
                 print(f"\tThroughput: {ips:.1f} img/s (job), {ips / self.ctx.world_size:.1f} img/s/GPU",
                       flush=True)
+                print(f"\tData wait (host blocked on input): {self.last_data_wait:.2f} seconds", flush=True)
                 if self.last_step_pct:
                     p = self.last_step_pct
                     print(f"\tStep time ms p50/p90/p99: {p[50]:.2f}/{p[90]:.2f}/{p[99]:.2f}", flush=True)
