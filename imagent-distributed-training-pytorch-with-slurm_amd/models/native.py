@@ -2,10 +2,13 @@
 
 ``bind_native(model, device, order)`` re-homes the parameters into a
 :class:`ParamArena` (fp32 master + grad + bf16 shadow, bucket order), builds
-the dgrad weight shadows (batched transpose plan), the padded stem weight
-(3 -> 8 input channels for 16-B NHWC loads) and one device workspace arena
-for every BatchNorm (conv-epilogue statistics, saved mean/invstd, backward
-scratch) that is zeroed with a single memset per training step.
+the dgrad weight shadows (batched transpose plan), the stem weight as rows of
+7 taps x 4 channels padded to 32 (``[Co][KH][32]``, the row-segment gather of
+a 4-channel NHWC input) and one device workspace arena for every BatchNorm
+(conv-epilogue statistics slab, backward reduction slab, saved mean/invstd)
+that is zeroed with a single memset per training step. Options: BN-backward
+fusion into the dgrad epilogue, weight gradients on a second stream, fp8
+forward (:class:`Fp8State`).
 """
 
 from __future__ import annotations
@@ -238,7 +241,7 @@ def _bn(x, bn, relu, train, x2=None, bn2=None, mode=0):
 
 
 def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
-    """x: NHWC bf16 [N, H, W, 8] (normalised, channels 3..7 zero) -> fp32 logits."""
+    """x: NHWC bf16 [N, H, W, 4] (normalised, channel 3 zero) -> fp32 logits."""
     st: NativeState = model.native
     if x.dtype != torch.bfloat16 or x.dim() != 4 or x.shape[-1] != ResNet.STEM_CPAD:
         raise ValueError(f"hip backend expects NHWC bf16 [N,H,W,{ResNet.STEM_CPAD}], got "
