@@ -234,8 +234,7 @@ def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
     side.wait_stream(torch.cuda.current_stream(dy.device))
     with torch.cuda.stream(side):
         _conv_wgrad(mod, dy, x)
-    dy.record_stream(side)
-    x.record_stream(side)
+    streams.protect(dy, x)
     streams.ensure_join_after_backward()
 
 

@@ -31,6 +31,10 @@ def set_wgrad_overlap(on: bool) -> None:
     _enabled = bool(on)
 
 
+def overlap_enabled() -> bool:
+    return _enabled
+
+
 def side_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.Stream]:
     """The wgrad stream of ``device`` (None when the overlap is off or on CPU)."""
     if not _enabled or not torch.cuda.is_available():
@@ -50,10 +54,30 @@ def active_side_stream() -> Optional[torch.cuda.Stream]:
     return _streams.get(torch.cuda.current_device())
 
 
+_keep: list = []
+
+
+def protect(*tensors: torch.Tensor) -> None:
+    """Keep tensors read on the side stream from being recycled too early:
+    ``record_stream`` in eager mode; while a HIP graph is being captured
+    (where ``record_stream`` is not usable) a reference is held until the
+    side stream has been joined back, which is also the dependency edge the
+    captured graph needs."""
+    s = active_side_stream()
+    if s is None:
+        return
+    if torch.cuda.is_current_stream_capturing():
+        _keep.extend(tensors)
+    else:
+        for t in tensors:
+            t.record_stream(s)
+
+
 def join_side_into_current() -> None:
     s = active_side_stream()
     if s is not None:
         torch.cuda.current_stream().wait_stream(s)
+    _keep.clear()
 
 
 _join_queued = False

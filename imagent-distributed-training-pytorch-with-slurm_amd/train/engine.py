@@ -125,8 +125,18 @@ class GraphedStep:
         self.static = [t.clone() for t in inputs]
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.fn(*self.static)
+        from ..ops import streams
+        # captured single-stream: capturing the weight-gradient side stream's
+        # fork/join (event edges between two streams) segfaults in
+        # hipStreamEndCapture on this ROCm 7 / torch 2.10 stack, even with the
+        # join made explicit -- measured, scripts/dev/graph_debug.py
+        overlap = streams.overlap_enabled()
+        streams.set_wgrad_overlap(False)
+        try:
+            with torch.cuda.graph(g):
+                self.fn(*self.static)
+        finally:
+            streams.set_wgrad_overlap(overlap)
         self.graph, self.key = g, key
         g.replay()  # the capture only recorded: run this step's work
         self.replays += 1
