@@ -94,6 +94,8 @@ def main(argv=None):
     comm = make_communicator(ctx, "rccl" if a.kernels == "hip" else "torch" if ctx.world_size > 1 else "local")
     ddp = DataParallel(model, arena, comm, bucket_cap_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                        rebuild_buckets=False)
+    if native is not None:  # compute shadows of the rank-0-broadcast masters
+        native.refresh_shadows(full=True)
     after = native.refresh_shadows if native else None
     if a.optimizer == "lars":
         from imagent_amd.train.optim import FlatLARS

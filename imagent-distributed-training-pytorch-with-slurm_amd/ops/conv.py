@@ -113,6 +113,13 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
     k = _lib.kernels()
     st = _lib.stream_ptr()
     S = stride
+    if not accumulate and S > 1 and (KH < S or KW < S):
+        # some parity classes get no tap (e.g. a strided 1x1): one memset of
+        # the output instead of zero-producing GEMM launches for those classes
+        out.zero_()
+        skip_empty = True
+    else:
+        skip_empty = accumulate
     for ph in range(S):
         for pw in range(S):
             gh = (H - ph + S - 1) // S  # rows of this parity class
@@ -123,10 +130,10 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             kw0 = (pw + pad) % S
             nth = max(0, (KH - kh0 + S - 1) // S)
             ntw = max(0, (KW - kw0 + S - 1) // S)
-            if accumulate and (nth == 0 or ntw == 0):
+            if skip_empty and (nth == 0 or ntw == 0):
                 if bnb is not None:
                     raise NotImplementedError("fused BN backward needs every parity class computed")
-                continue  # no tap reaches this parity class: nothing to add
+                continue  # no tap reaches this parity class: zero / nothing to add
             a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
                            KH * KW * Co, 1)
             a.nth, a.ntw = nth, ntw

@@ -248,6 +248,8 @@ class Trainer:
         self.ddp = DataParallel(model, arena, self.comm, bucket_cap_mb=a.bucket_mb,
                                 first_bucket_mb=a.first_bucket_mb, broadcast_buffers=a.broadcast_buffers,
                                 rebuild_buckets=a.rebuild_buckets)
+        if self.native is not None:  # the rank-0 broadcast may have rewritten the fp32 masters
+            self.native.refresh_shadows(full=True)
         after = self.native.refresh_shadows if self.native else None
         full = (lambda: self.native.refresh_shadows(full=True)) if self.native else None
         self.opt = build_optimizer(a.optimizer, arena, a.lr, a.momentum, a.wd, a.nesterov,
