@@ -170,6 +170,9 @@ def main(argv=None):
                 "grad_allreduce": "fp32 bucketed RCCL avg, side stream",
                 "bucket_mb": a.bucket_mb,
                 "mean_train_loss": round(loss, 4),
+                "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
+                "alloc_retries": int(torch.cuda.memory_stats(dev).get("num_alloc_retries", 0))
+                if dev.type == "cuda" else None,
             },
         }
         print(json.dumps(out), flush=True)

@@ -29,6 +29,28 @@ namespace {
 constexpr int U = 4;  // rows per thread per loop iteration (loads batched ahead of the math)
 constexpr int BWD_SLOTS = 32;  // backward reduction slab slots
 
+// optional e5m2 copies of the backward outputs (dx, dx2) for the fp8 dgrad
+// (conv_igemm_fp8.hip, IG_BF8X), quantised with 2^-exp and amax-tracked in
+// 32-slot rows (folded by imk_fp8_update_exp): delayed scaling as forward
+struct G8Out {
+    uint32_t* q[2];
+    const int* exp[2];
+    float* amax[2];
+};
+
+constexpr float E5M2_MAX = 57344.f;
+
+__device__ __forceinline__ uint32_t pack4_bf8(float a, float b, float c, float d) {
+    a = fminf(fmaxf(a, -E5M2_MAX), E5M2_MAX);
+    b = fminf(fmaxf(b, -E5M2_MAX), E5M2_MAX);
+    c = fminf(fmaxf(c, -E5M2_MAX), E5M2_MAX);
+    d = fminf(fmaxf(d, -E5M2_MAX), E5M2_MAX);
+    int w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+    return (uint32_t)w;
+}
+
+
 struct Vec8 {
     float v[8];
 };
@@ -57,6 +79,26 @@ __device__ __forceinline__ void st8(bf16_t* p, const Vec8& x) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = pack_bf2(x.v[2 * i], x.v[2 * i + 1]);
     *reinterpret_cast<u32x4*>(p) = w;
+}
+
+// store the bf16 row chunk; with q: also its e5m2 copy, track |.| max in m
+__device__ __forceinline__ void st8_q(bf16_t* p, const Vec8& x, uint32_t* q, size_t off, float s, float& m) {
+    u32x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf2(x.v[2 * i], x.v[2 * i + 1]);
+    *reinterpret_cast<u32x4*>(p) = w;
+    if (q) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = lo_bf(w[i]);
+            v[2 * i + 1] = hi_bf(w[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
+        reinterpret_cast<u32x2*>(q)[off / 8] =
+            u32x2{pack4_bf8(v[0] * s, v[1] * s, v[2] * s, v[3] * s), pack4_bf8(v[4] * s, v[5] * s, v[6] * s, v[7] * s)};
+    }
 }
 
 // mean / invstd from conv-epilogue sums
@@ -311,8 +353,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ scratch, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
     const bf16_t* __restrict__ x2, const float* __restrict__ save2, const float* __restrict__ gamma2,
     bf16_t* __restrict__ dx2, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt) {
+    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8) {
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
+    const float qs0 = g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
+    const float qs1 = g8.q[1] ? ldexpf(1.f, -g8.exp[1][0]) : 0.f;
+    float m0 = 0.f, m1 = 0.f;
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
             if (dgamma) dgamma[c] += scratch[c];
@@ -372,15 +417,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             Vec8 o;
 #pragma unroll
             for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g[u].v[i] + k2[i] + k3[i] * (xv[u].v[i] - mean[i]);
-            st8(dx + off, o);
+            st8_q(dx + off, o, g8.q[0], off, qs0, m0);
             if (MODE == 1) st8(dres + off, g[u]);
             if (MODE == 2) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     o.v[i] = q1[i] * g[u].v[i] + q2[i] + q3[i] * (x2v[u].v[i] - m2[i]);
-                st8(dx2 + off, o);
+                st8_q(dx2 + off, o, g8.q[1], off, qs1, m1);
             }
         }
+    }
+    if (g8.q[0] || g8.q[1]) {  // every lane active (host check): block max -> slot (blockIdx & 31)
+        __shared__ float wm[2][4];
+        m0 = wave_max(m0);
+        m1 = wave_max(m1);
+        if ((tid & 63) == 0) {
+            wm[0][tid >> 6] = m0;
+            wm[1][tid >> 6] = m1;
+        }
+        __syncthreads();
+        if (tid < 2 && g8.q[tid])
+            atomic_max_pos(g8.amax[tid] + (blockIdx.x & 31),
+                           fmaxf(fmaxf(wm[tid][0], wm[tid][1]), fmaxf(wm[tid][2], wm[tid][3])));
     }
 }
 
@@ -434,8 +492,21 @@ IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
 IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save, const float* gamma,
                                 const void* x2, const float* save2, const float* gamma2, float* scratch,
                                 void* dx, void* dx2, float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
-                                float* dbeta2_acc, long R, int C, int mode, void* stream) {
+                                float* dbeta2_acc, long R, int C, int mode, const void* g8desc, void* stream) {
     if (C % 8 || C > 2048) return -100;
+    // g8desc (host pointer, may be null): {q0, q1, exp0, exp1, amax0, amax1} device pointers of the
+    // e5m2 copies of dx / dx2 (fp8 dgrad)
+    G8Out g8{};
+    if (g8desc) {
+        const void* const* d = static_cast<const void* const*>(g8desc);
+        g8.q[0] = (uint32_t*)d[0];
+        g8.q[1] = (uint32_t*)d[1];
+        g8.exp[0] = (const int*)d[2];
+        g8.exp[1] = (const int*)d[3];
+        g8.amax[0] = (float*)d[4];
+        g8.amax[1] = (float*)d[5];
+        if ((g8.q[0] || g8.q[1]) && 256 % (C / 8)) return -102;
+    }
     hipStream_t st = (hipStream_t)stream;
     float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
     hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
@@ -447,7 +518,7 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)g,   \
                        nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr, \
                        (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,         \
-                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
+                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8)
     if (mode == 2) LA(2); else LA(0);
 #undef LA
     IMK_CHECK_LAUNCH();
@@ -495,7 +566,7 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
                        (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, folded, (bf16_t*)dx,   \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
-                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt)
+                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{})
     if (mode == 0) { if (relu == 2) LA(2, 0); else if (relu) LA(1, 0); else LA(0, 0); }
     else if (mode == 1) { if (relu) LA(1, 1); else LA(0, 1); }
     else { if (relu) LA(1, 2); else LA(0, 2); }

@@ -71,6 +71,8 @@ struct QDesc {
     long n4;           // elements / 4
     int* exp;          // per-tensor exponent (written)
     float* amax;       // per-tensor scratch (zeroed by the caller)
+    uint8_t* dstT;     // optional e4m3 copy of a conv weight [Co][T][Ci] transposed to [Ci][T][Co] (dgrad)
+    int T, Ci;
 };
 
 // pass 1: per-tensor amax (blockIdx.y = tensor)
@@ -91,9 +93,21 @@ __global__ __launch_bounds__(256) void weight_quant_kernel(const QDesc* __restri
     const int e = exp_for(q.amax[0], margin);
     if (blockIdx.x == 0 && threadIdx.x == 0) q.exp[0] = e;
     const float s = ldexpf(1.f, -e);
+    const long tc = (long)q.T * q.Ci;
+    const long Co = q.dstT ? q.n4 * 4 / tc : 0;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < q.n4; i += (long)gridDim.x * 256) {
         const f32x4 v = reinterpret_cast<const f32x4*>(q.src)[i];
-        q.dst[i] = pack4_fp8(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+        const uint32_t w = pack4_fp8(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+        q.dst[i] = w;
+        if (q.dstT) {  // element e = 4i + j of [Co][T][Ci] -> [Ci][T][Co]
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const long e = 4 * i + j;
+                const long co = e / tc, rem = e - co * tc;
+                const long t = rem / q.Ci, ci = rem - t * q.Ci;
+                q.dstT[(ci * q.T + t) * Co + co] = (uint8_t)(w >> (8 * j));
+            }
+        }
     }
 }
 

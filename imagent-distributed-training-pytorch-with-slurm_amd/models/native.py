@@ -169,18 +169,25 @@ class Fp8State:
     (delayed per-tensor scales, written by the producing BN / pool). The
     backward stays bf16 (bf16 weight shadows, bf16 saved activations)."""
 
-    def __init__(self, st: "NativeState"):
-        from ..ops.fp8 import ActScales, WeightQuantizer
+    def __init__(self, st: "NativeState", backward: bool = True):
+        from ..ops.fp8 import E5M2_MAX, ActScales, WeightQuantizer
         m = st.model
         convs = [c for c in m.convs() if c is not m.conv1]
-        self.wq = WeightQuantizer([c.weight for c in convs], st.device)
-        for c, v, i in zip(convs, self.wq.views, range(len(convs))):
+        self.wq = WeightQuantizer([c.weight for c in convs], st.device, transposed=backward)
+        for c, v, vt, i in zip(convs, self.wq.views, self.wq.views_t, range(len(convs))):
             c.w8 = v.view(c.out_channels, c.kh, c.kw, c.in_channels)
+            c.wt8 = vt  # [Ci][KH][KW][Co] e4m3 (fp8 dgrad) or None
             c.w8_exp = self.wq.exp[i:i + 1]
         bns = m.batchnorms()
         self.slot = {id(bn): i for i, bn in enumerate(bns)}
         self.pool_slot = len(bns)
         self.act = ActScales(len(bns) + 1, st.device)
+        # e5m2 copies of the BN-backward outputs (the dgrad inputs), delayed
+        # scaling; the first step only observes (bf16 dgrad) so the initial
+        # exponent never has to guess the gradient magnitude
+        self.backward = backward
+        self.grad = ActScales(len(bns), st.device, fmt_max=E5M2_MAX) if backward else None
+        self.grad_ready = False
         self.map = {}
         self.active = False
         self.wq.run()
@@ -189,6 +196,17 @@ class Fp8State:
         """Masters changed: re-quantise weights; this step's amax -> next exponents."""
         self.wq.run()
         self.act.step()
+        if self.grad is not None:
+            self.grad.step()
+            self.grad_ready = True
+
+    def grad_out(self, like: torch.Tensor, bn):
+        """(e5m2 buffer, exponent view, amax row) for a BN-backward output, or None."""
+        if self.grad is None or like.shape[-1] % 16 or 256 % (like.shape[-1] // 8):
+            return None
+        i = self.slot[id(bn)]
+        return (torch.empty(like.shape, dtype=torch.uint8, device=like.device), self.grad.exp[i:i + 1],
+                self.grad.amax[i])
 
     def begin_forward(self) -> None:
         self.map.clear()

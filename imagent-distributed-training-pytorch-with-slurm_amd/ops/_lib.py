@@ -99,7 +99,7 @@ class LarsDesc(C.Structure):
 class QDesc(C.Structure):
     """fp8.hip QDesc: one weight tensor of the per-step e4m3 quantisation."""
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("n4", C.c_long), ("exp", C.c_void_p),
-                ("amax", C.c_void_p)]
+                ("amax", C.c_void_p), ("dstT", C.c_void_p), ("T", C.c_int), ("Ci", C.c_int)]
 
 
 class WgradArgs(C.Structure):
@@ -137,7 +137,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
                            vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
-            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp],
+            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],

@@ -45,6 +45,18 @@ def _fwd8(conv, h, h8, bn):
                      fp8=(h8[1], conv.w8_exp))
 
 
+def _use8(q, g8):
+    """The e5m2 copy a BN-backward pass wrote, once gradient scales exist."""
+    return (g8[0], g8[1]) if (g8 is not None and q.grad_ready) else None
+
+
+def _dg8(d8, conv):
+    """fp8 dgrad operands (e5m2 gradient, e4m3 transposed weights) or None (bf16)."""
+    if d8 is None or getattr(conv, "wt8", None) is None or conv.out_channels % 16:
+        return None
+    return (d8[0], d8[1], conv.wt8, conv.w8_exp)
+
+
 class BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, block):
@@ -90,6 +102,9 @@ class BlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         block = ctx.block
         pairs = block.convs_bns()
+        q = getattr(block, "_q8", None)  # Fp8State: e5m2 BN-backward outputs feed fp8 dgrads
+        if q is not None and not q.backward:
+            q = None
         t = ctx.saved_tensors
         x = t[0]
         n = len(pairs)
@@ -104,16 +119,24 @@ class BlockFn(torch.autograd.Function):
         ds = block.downsample
         fuse = getattr(block, "_fuse_bnb", False)
         premasked = getattr(block, "_bnb_done", False)
+        dA8 = None
         if ds is not None:
             if premasked:  # dout already masked + reduced by the next block's conv1 dgrad
-                dA, dAd = bn_apply_backward(dout, a_last, ad, bn_l, ds[1], 2)
+                g8a = q.grad_out(a_last, bn_l) if q is not None else None
+                g8b = q.grad_out(ad, ds[1]) if q is not None else None
+                dA, dAd = bn_apply_backward(dout, a_last, ad, bn_l, ds[1], 2, g8=(g8a, g8b))
+                dA8, dAd8 = _use8(q, g8a), _use8(q, g8b)
             else:
                 dA, dAd = bn_act_backward(dout, a_last, ad, out, bn_l, ds[1], 2, True)
+                dAd8 = None
             dconv = ds[0]
-            dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw)
+            dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw,
+                             fp8=_dg8(dAd8, dconv))
             conv_wgrad(dconv, dAd, x)
         elif premasked:
-            dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1)
+            g8a = q.grad_out(a_last, bn_l) if q is not None else None
+            dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
+            dA8 = _use8(q, g8a)
             dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
         else:
             dA, dX = bn_act_backward(dout, a_last, x, out, bn_l, None, 1, True)  # dX = masked dout
@@ -126,12 +149,15 @@ class BlockFn(torch.autograd.Function):
                 bn_prev = pairs[i - 1][1]
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 dH = igemm_dgrad(dA, conv.wt_bf16, (h_in.shape[1], h_in.shape[2]), conv.stride, conv.padding,
-                                 conv.kh, conv.kw, bnb=fz)
+                                 conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
                 conv_wgrad(conv, dA, h_in)
                 if fz is not None:
-                    dA, _ = bn_apply_backward(dH, acts[i - 1], None, bn_prev, None, 0)
+                    g8a = q.grad_out(acts[i - 1], bn_prev) if q is not None else None
+                    dA, _ = bn_apply_backward(dH, acts[i - 1], None, bn_prev, None, 0, g8=(g8a, None))
+                    dA8 = _use8(q, g8a)
                 else:
                     dA, _ = bn_act_backward(dH, acts[i - 1], None, None, bn_prev, None, 0, True)
+                    dA8 = None
             else:
                 prev = getattr(block, "_prev_block", None)
                 fz = None
@@ -141,7 +167,7 @@ class BlockFn(torch.autograd.Function):
                     pds = prev.downsample
                     fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
-                            accumulate=True, bnb=fz)
+                            accumulate=True, bnb=fz, fp8=_dg8(dA8, conv))
                 conv_wgrad(conv, dA, h_in)
                 if fz is not None:
                     prev._bnb_done = True

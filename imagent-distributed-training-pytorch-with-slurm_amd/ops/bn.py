@@ -13,6 +13,7 @@ Three forms cover torchvision's blocks (reference model: ``imagenet.py:312``):
 
 from __future__ import annotations
 
+import ctypes as C
 from typing import Optional, Tuple
 
 import torch
@@ -89,11 +90,13 @@ def bn_act_backward(dy: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor
 
 
 def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2,
-                      mode: int) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                      mode: int, g8=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Backward of act(bn(x) [+ res | + bn2(x2)]) for a gradient ``g`` that its
     producing dgrad already ReLU-masked and reduced into ``bn.work.scratch``
     (``ops.conv.BNBwdFuse``): one fold + one streaming apply pass.
-    Returns (dx, dx2 | None); for mode 1 the residual-branch gradient is g."""
+    Returns (dx, dx2 | None); for mode 1 the residual-branch gradient is g.
+    ``g8 = ((q, exp, amax) | None, (q2, exp2, amax2) | None)``: also write e5m2
+    copies of dx / dx2 for the fp8 dgrad (``Fp8State``)."""
     w = bn.work
     C = x.shape[-1]
     R = x.numel() // C
@@ -104,13 +107,25 @@ def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tenso
         bn2.work.save.data_ptr() if mode == 2 else 0, bn2.weight.data_ptr() if mode == 2 else 0,
         w.scratch.data_ptr(), dx.data_ptr(), _lib.ptr(dx2), bn.weight.grad.data_ptr(),
         bn.bias.grad.data_ptr(), bn2.weight.grad.data_ptr() if mode == 2 else 0,
-        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _lib.stream_ptr()), "bn bwd apply")
+        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _g8desc(g8), _lib.stream_ptr()),
+        "bn bwd apply")
     notify_ready(bn.weight)
     notify_ready(bn.bias)
     if mode == 2:
         notify_ready(bn2.weight)
         notify_ready(bn2.bias)
     return dx, dx2
+
+
+def _g8desc(g8):
+    if g8 is None or (g8[0] is None and g8[1] is None):
+        return None
+    a, b = g8
+    arr = (C.c_void_p * 6)(_lib.ptr(a[0]) if a else 0, _lib.ptr(b[0]) if b else 0,
+                           _lib.ptr(a[1]) if a else 0, _lib.ptr(b[1]) if b else 0,
+                           _lib.ptr(a[2]) if a else 0, _lib.ptr(b[2]) if b else 0)
+    _g8desc.keep = arr  # alive until the (synchronous) launch call returns
+    return C.cast(arr, C.c_void_p)
 
 
 class BNActFn(torch.autograd.Function):

@@ -92,7 +92,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
 def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
                 KH: int, KW: int, out: Optional[torch.Tensor] = None,
                 accumulate: bool = False, tile: int = 0, bnb: Optional["BNBwdFuse"] = None,
-                epi: int = 0) -> torch.Tensor:
+                epi: int = 0, fp8=None) -> torch.Tensor:
     """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci,KH,KW,Co]).
 
     Stride 1: one gather-GEMM launch with the taps mirrored.
@@ -103,6 +103,8 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
     ``bnb``: ``dx`` is the upstream gradient of that BatchNorm(+add)+ReLU: the
     epilogue stores it ReLU-masked and adds the BN-backward reductions to the
     BN's slab (finish with :func:`ops.bn.bn_apply_backward`).
+    ``fp8 = (dy8, exp_dy, wt8, exp_w)``: e5m2 gradient x e4m3 transposed
+    weights on the block-scaled MFMA (device int32 exponents).
     """
     assert not accumulate or out is not None
     N, OH, OW, Co = dy.shape
@@ -134,14 +136,19 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
                 if bnb is not None:
                     raise NotImplementedError("fused BN backward needs every parity class computed")
                 continue  # no tap reaches this parity class: zero / nothing to add
-            a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
-                           KH * KW * Co, 1)
+            if fp8 is None:
+                a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
+                               KH * KW * Co, 1)
+            else:
+                a = _base_args(fp8[0].data_ptr(), fp8[2].data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci,
+                               KH * KW * Co, 1)
+                a.xexp, a.wexp = fp8[1].data_ptr(), fp8[3].data_ptr()
             a.nth, a.ntw = nth, ntw
             a.dh0, a.dhs = (ph + pad - kh0) // S, -1
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi]
+            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi] | (256 | 512 if fp8 is not None else 0)
             if bnb is not None:
                 bnb.fill(a)
             _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")

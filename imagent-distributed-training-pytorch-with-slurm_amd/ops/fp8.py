@@ -21,6 +21,7 @@ import torch
 from . import _lib
 
 E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
 AMAX_SLOTS = 32  # fp8.hip / bn.hip: per-tensor amax row, folded by imk_fp8_update_exp
 
 
@@ -36,26 +37,33 @@ def quant_act(x: torch.Tensor, exp: torch.Tensor, amax: torch.Tensor = None,
 
 
 class ActScales:
-    """Device exponents + amax accumulators for ``n`` activation tensors."""
+    """Device exponents + amax accumulators for ``n`` activation (or gradient) tensors."""
 
-    def __init__(self, n: int, device, margin: int = 0):
+    def __init__(self, n: int, device, margin: int = 0, fmt_max: float = E4M3_MAX, init_exp: int = 0):
         self.n = n
-        self.exp = torch.zeros(n, dtype=torch.int32, device=device)
+        self.exp = torch.full((n,), init_exp, dtype=torch.int32, device=device)
+        self.fmt_max = fmt_max
         self.amax = torch.zeros(n, AMAX_SLOTS, dtype=torch.float32, device=device)  # spread atomics
         self.margin = margin
 
     def step(self) -> None:
+        # the kernel sizes exponents for e4m3 (448); e5m2's 57344 = 448 * 2^7
+        extra = 0 if self.fmt_max == E4M3_MAX else -7
         _lib.check(_lib.kernels().imk_fp8_update_exp(self.amax.data_ptr(), self.exp.data_ptr(), self.n,
-                                                     self.margin, _lib.stream_ptr()), "fp8 update exp")
+                                                     self.margin + extra, _lib.stream_ptr()), "fp8 update exp")
 
 
 class WeightQuantizer:
     """e4m3 shadows of fp32 weights, re-quantised (exact amax) by :meth:`run`."""
 
-    def __init__(self, weights: Sequence[torch.Tensor], device, margin: int = 0):
+    def __init__(self, weights: Sequence[torch.Tensor], device, margin: int = 0, transposed: bool = False):
+        """``transposed``: also keep [Ci][KH][KW][Co] copies (``views_t``) of
+        4-d conv weights for the fp8 dgrad, same per-tensor exponent."""
         dev = torch.device(device)
         total = sum((w.numel() + 15) // 16 * 16 for w in weights)
         self.q = torch.zeros(total, dtype=torch.uint8, device=dev)
+        self.qt = torch.zeros(total, dtype=torch.uint8, device=dev) if transposed else None
+        self.views_t: List[torch.Tensor] = []
         self.exp = torch.zeros(len(weights), dtype=torch.int32, device=dev)
         self.amax = torch.zeros(len(weights), dtype=torch.float32, device=dev)
         self.views: List[torch.Tensor] = []
@@ -68,6 +76,13 @@ class WeightQuantizer:
             self.views.append(v)
             d = descs[i]
             d.src, d.dst, d.n4 = w.data_ptr(), v.data_ptr(), w.numel() // 4
+            if self.qt is not None and w.dim() == 4:
+                co, ci, kh, kw = w.shape
+                vt = self.qt[off:off + w.numel()]
+                self.views_t.append(vt.view(ci, kh, kw, co))
+                d.dstT, d.T, d.Ci = vt.data_ptr(), kh * kw, ci
+            else:
+                self.views_t.append(None)
             d.exp = self.exp[i:i + 1].data_ptr()
             d.amax = self.amax[i:i + 1].data_ptr()
             max_n4 = max(max_n4, w.numel() // 4)

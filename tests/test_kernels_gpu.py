@@ -402,3 +402,33 @@ def test_lars_native_matches_cpu_math():
         oc.step()
     assert torch.allclose(ar_g.P.cpu(), ar_c.P, rtol=1e-4, atol=1e-6)
     assert torch.equal(ar_g.S.cpu(), ar_g.P.cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("accum", [False, True])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 2, 0), (3, 128, 12, 64, 3, 2, 1),
+                                   (2, 512, 7, 256, 1, 1, 0)])
+def test_conv_fp8_dgrad(shape, accum):
+    """e5m2 gradient x e4m3 transposed weights (IG_FP8 | IG_BF8X) vs the fp32
+    dgrad of the dequantised operands, incl. strided parity classes and the
+    residual-accumulating epilogue."""
+    from imagent_amd.ops.conv import igemm_dgrad
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(13)
+    eg, ew = -14, -9
+    w = torch.randn(Co, Ci, k, k, device=DEV) * 0.05
+    OH = (H + 2 * p - k) // s + 1
+    g = torch.randn(N, Co, OH, OH, device=DEV) * 1e-3
+    g8 = (g * 2.0 ** -eg).clamp(-57344, 57344).to(torch.float8_e5m2)
+    w8 = (w * 2.0 ** -ew).clamp(-448, 448).to(torch.float8_e4m3fn)
+    gd, wd = g8.float() * 2.0 ** eg, w8.float() * 2.0 ** ew
+    xr = torch.zeros(N, Ci, H, H, device=DEV, requires_grad=True)
+    F.conv2d(xr, wd, None, s, p).backward(gd)
+    e = torch.tensor([eg, ew], dtype=torch.int32, device=DEV)
+    wt8 = w8.view(torch.uint8).permute(1, 2, 3, 0).contiguous()  # [Ci][KH][KW][Co]
+    dy_bf = nhwc(bf(gd))  # the bf16 operand only provides shapes here
+    base = bf(torch.randn(N, H, H, Ci, device=DEV) * 1e-3) if accum else None
+    out = base.clone() if accum else None
+    dx = igemm_dgrad(dy_bf, wt8, (H, H), s, p, k, k, out=out, accumulate=accum,
+                     fp8=(nhwc(g8.view(torch.uint8)), e[0:1], wt8, e[1:2]))
+    ref = nhwc(xr.grad) + (base.float() if accum else 0)
+    assert rel(dx, ref) < 1e-2
