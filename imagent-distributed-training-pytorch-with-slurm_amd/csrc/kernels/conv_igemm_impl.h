@@ -92,6 +92,7 @@ struct IGemmArgs {
 #define IG_EPI_DIRECT 128  // direct register epilogue even for IG_BNBWD (A/B testing)
 #define IG_FP8 256     // fp8 operands on the block-scaled MFMA (conv_igemm_fp8.hip)
 #define IG_BF8X 512    // with IG_FP8: the gathered operand X is e5m2 (gradients), Wk e4m3
+#define IG_AFFINE 1024 // inference BN folded into the epilogue: out = acc * bias[n] + bias[Nout + n]
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 static __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes (per TU)
@@ -200,7 +201,11 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 v[r] = acc[i][j][r];
-                if (a.bias) v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
+                if (a.flags & IG_AFFINE) {  // folded inference BN: bias = [scale | shift]
+                    if (n + r < a.Nout) v[r] = fmaf(v[r], a.bias[n + r], a.bias[a.Nout + n + r]);
+                } else if (a.bias) {
+                    v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
+                }
             }
             if (out_f32) {
                 float* y = reinterpret_cast<float*>(a.Y) + pix * a.ldy + n;

@@ -270,6 +270,8 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     q = st.fp8 if (train and st.fused_blocks) else None
     if q is not None:
         q.begin_forward()
+    if not train:
+        return _forward_eval(model, x)
     rows = []
     y = _conv(x, model.conv1, model.bn1, train)
     rows.append(y.numel() // y.shape[-1])
@@ -315,6 +317,42 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
         logits = igemm_fwd(pooled.view(B, 1, 1, -1), fc.w_bf16.view(fc.out_features, 1, 1, -1), 1, 0, 1,
                            1, bias=fc.bias, out_f32=True).view(B, -1)
     return logits
+
+
+def _affine(bn: BatchNorm2d) -> torch.Tensor:
+    """Inference BN as a per-channel [scale; shift] for the conv epilogue (IG_AFFINE)."""
+    with torch.no_grad():
+        sc = bn.weight * torch.rsqrt(bn.running_var + bn.eps)
+        return torch.stack([sc, bn.bias - bn.running_mean * sc]).float().contiguous()
+
+
+def _forward_eval(model: ResNet, x: torch.Tensor) -> torch.Tensor:
+    """Inference: every BatchNorm (+ReLU, +residual) folded into the epilogue
+    of the conv that feeds it -- one pass per conv, no BN kernels.
+    The block's last conv accumulates onto the shortcut (identity copy or the
+    downsample conv's folded output) and applies the ReLU after the sum."""
+    def conv(h, c, bn, relu, out=None, accumulate=False):
+        return igemm_fwd(h, c.w_bf16, c.stride, c.padding, c.kh, c.kw, stem=getattr(c, "stem", False),
+                         affine=_affine(bn), relu=relu, out=out, accumulate=accumulate)
+
+    y = conv(x, model.conv1, model.bn1, True)
+    y = maxpool_eval(y, 3, 2, 1)
+    for b in model.blocks():
+        pairs = b.convs_bns()
+        h = y
+        for c, bn, _ in pairs[:-1]:
+            h = conv(h, c, bn, True)
+        c, bn, _ = pairs[-1]
+        if b.downsample is not None:
+            short = conv(y, b.downsample[0], b.downsample[1], False)
+        else:
+            short = y.clone()
+        y = conv(h, c, bn, True, out=short, accumulate=True)
+    pooled = _avg_eval(y)
+    fc = model.fc
+    B = pooled.shape[0]
+    return igemm_fwd(pooled.view(B, 1, 1, -1), fc.w_bf16.view(fc.out_features, 1, 1, -1), 1, 0, 1, 1,
+                     bias=fc.bias, out_f32=True).view(B, -1)
 
 
 def _avg_eval(y):

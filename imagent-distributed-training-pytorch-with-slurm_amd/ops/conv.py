@@ -54,7 +54,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
               stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
               tile: int = 0, stem: bool = False, epi: int = 0,
-              fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+              fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, affine: Optional[torch.Tensor] = None,
+              accumulate: bool = False) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` [2, Co].
 
@@ -62,7 +63,9 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     channels, zero padded) - the row-segment gather of the 7x7 stem.
     ``fp8 = (ex, ew)``: x and w are e4m3 bytes (uint8) holding x*2^-ex and
     w*2^-ew, ex/ew device int32 scalars; the block-scaled MFMA restores the
-    scales (Ci % 16 == 0)."""
+    scales (Ci % 16 == 0).
+    ``affine`` [2, Co] fp32 (scale, shift): an inference BatchNorm folded into
+    the epilogue (before ``accumulate`` into ``out`` and ``relu``)."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
@@ -76,7 +79,12 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = KH, KW, -pad, 1, -pad, 1
     a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
-    a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0) | _EPI_FLAGS[epi]
+    a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0) | _EPI_FLAGS[epi] | \
+        (8 if accumulate else 0)
+    if affine is not None:
+        assert bias is None and affine.shape == (2, Co) and affine.dtype == torch.float32
+        a.flags |= 1024
+        a.bias = affine.data_ptr()
     if fp8 is not None:
         assert x.dtype == torch.uint8 and w.dtype == torch.uint8, (x.dtype, w.dtype)
         a.flags |= 256
