@@ -36,9 +36,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
                    help="compute dtype. HIP kernels: bf16 (fp32 masters/accumulation), or fp8 = e4m3 "
                         "forward convs on the block-scaled MFMA with bf16 backward; fp32 = torch oracle path")
-    p.add_argument("--data", default="imagenet", choices=["imagenet", "synthetic"])
+    p.add_argument("--data", default="imagenet", choices=["imagenet", "records", "synthetic"],
+                   help="imagenet: JPEG folders decoded by worker processes; records: train.imrec / val.imrec "
+                        "(python -m imagent_amd.data.records) gathered by the native thread pool")
     p.add_argument("--data-root", default=None, help="default: <cwd>/../data/imagenet (imagenet.py:287)")
-    p.add_argument("--workers", type=int, default=10)
+    p.add_argument("--workers", type=int, default=10, help="decode processes (imagenet) / gather threads (records)")
     p.add_argument("--num-classes", type=int, default=1000, help="synthetic data only")
     p.add_argument("--synthetic-train-size", type=int, default=1281167)
     p.add_argument("--synthetic-val-size", type=int, default=50000)

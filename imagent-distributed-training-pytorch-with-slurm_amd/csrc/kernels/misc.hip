@@ -20,20 +20,24 @@ namespace {
 // ------------------------------------------------------------------ maxpool
 // argmax stored per element as the in-window index (uint8), so the backward
 // is a gather over the <= ceil(k/s)^2 windows that contain an input pixel.
+// Flat grid-stride over (pixel, 8-channel chunk) with 32-bit unsigned index
+// math. Every window's loads are issued before any is used, from clamped
+// (always valid) addresses with the validity kept as a mask: the
+// branch-per-window form waits one L2 round trip per window (the stem's pool
+// backward measured 594 us, 4x its bytes; profiles/r50_b512_v5_kernel_stats.md).
+template <int KMAX>  // KMAX > 0: k <= KMAX, windows unrolled; 0: generic k
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
                                                           int W, int C, int OH, int OW, int k, int s,
                                                           int p) {
-    const int cpr = C / 8;
-    const long total = (long)N * OH * OW * cpr;
-    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
-        const int ch = t % cpr;
-        long pix = t / cpr;
-        const int ow = pix % OW;
-        pix /= OW;
-        const int oh = pix % OH;
-        const int n = pix / OH;
+    const uint32_t cpr = C / 8;
+    const uint32_t total = (uint32_t)N * OH * OW * cpr;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+        const uint32_t pix = t / cpr, ch = t - pix * cpr;
+        const uint32_t row = pix / (uint32_t)OW, ow = pix - row * OW;
+        const uint32_t n = row / (uint32_t)OH, oh = row - n * OH;
+        const bf16_t* xn = x + (size_t)n * H * W * C + ch * 8;
         float best[8];
         int bi[8];
 #pragma unroll
@@ -41,20 +45,40 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
             best[i] = -INFINITY;
             bi[i] = 0;
         }
-        for (int dh = 0; dh < k; ++dh) {
-            const int ih = oh * s - p + dh;
-            if ((unsigned)ih >= (unsigned)H) continue;
-            for (int dw = 0; dw < k; ++dw) {
-                const int iw = ow * s - p + dw;
-                if ((unsigned)iw >= (unsigned)W) continue;
-                const u32x4 w =
-                    *reinterpret_cast<const u32x4*>(x + (((size_t)n * H + ih) * W + iw) * C + ch * 8);
+        auto take = [&](const u32x4& w, bool ok, int win) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float a = lo_bf(w[i]), b = hi_bf(w[i]);
-                    // strict > keeps the first maximum (torch semantics); NaN propagates
-                    if (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i])) { best[2 * i] = a; bi[2 * i] = dh * k + dw; }
-                    if (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1])) { best[2 * i + 1] = b; bi[2 * i + 1] = dh * k + dw; }
+            for (int i = 0; i < 4; ++i) {
+                const float a = lo_bf(w[i]), b = hi_bf(w[i]);
+                // strict > keeps the first maximum (torch semantics); NaN propagates
+                if (ok && (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i]))) { best[2 * i] = a; bi[2 * i] = win; }
+                if (ok && (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1]))) { best[2 * i + 1] = b; bi[2 * i + 1] = win; }
+            }
+        };
+        if constexpr (KMAX > 0) {
+            constexpr int KK = KMAX > 0 ? KMAX * KMAX : 1;
+            u32x4 v[KK];
+            bool ok[KK];
+#pragma unroll
+            for (int dh = 0; dh < KMAX; ++dh)
+#pragma unroll
+                for (int dw = 0; dw < KMAX; ++dw) {
+                    const int ih = (int)oh * s - p + dh, iw = (int)ow * s - p + dw;
+                    ok[dh * KMAX + dw] = dh < k && dw < k && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+                    const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+                    v[dh * KMAX + dw] = *reinterpret_cast<const u32x4*>(xn + ((size_t)ihc * W + iwc) * C);
+                }
+#pragma unroll
+            for (int dh = 0; dh < KMAX; ++dh)
+#pragma unroll
+                for (int dw = 0; dw < KMAX; ++dw) take(v[dh * KMAX + dw], ok[dh * KMAX + dw], dh * k + dw);
+        } else {
+            for (int dh = 0; dh < k; ++dh) {
+                const int ih = (int)oh * s - p + dh;
+                if ((unsigned)ih >= (unsigned)H) continue;
+                for (int dw = 0; dw < k; ++dw) {
+                    const int iw = (int)ow * s - p + dw;
+                    if ((unsigned)iw >= (unsigned)W) continue;
+                    take(*reinterpret_cast<const u32x4*>(xn + ((size_t)ih * W + iw) * C), true, dh * k + dw);
                 }
             }
         }
@@ -67,53 +91,78 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
             i0 |= (uint32_t)bi[i] << (8 * i);
             i1 |= (uint32_t)bi[4 + i] << (8 * i);
         }
-        const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + ch * 8;
+        const size_t off = (size_t)pix * C + ch * 8;
         *reinterpret_cast<u32x4*>(y + off) = o;
         if (idx) *reinterpret_cast<u32x2*>(idx + off) = u32x2{i0, i1};
     }
 }
 
+// WMAX > 0: at most WMAX candidate windows per dimension (ceil(k/s) <= WMAX),
+// unrolled; 0: generic
+template <int WMAX>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           bf16_t* __restrict__ dx, int N, int H, int W,
                                                           int C, int OH, int OW, int k, int s, int p) {
-    const int cpr = C / 8;
-    const long total = (long)N * H * W * cpr;
-    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
-        const int ch = t % cpr;
-        long pix = t / cpr;
-        const int iw = pix % W;
-        pix /= W;
-        const int ih = pix % H;
-        const int n = pix / H;
+    const uint32_t cpr = C / 8;
+    const uint32_t total = (uint32_t)N * H * W * cpr;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+        const uint32_t pix = t / cpr, ch = t - pix * cpr;
+        const uint32_t row = pix / (uint32_t)W, iw = pix - row * W;
+        const uint32_t n = row / (uint32_t)H, ih = row - n * H;
+        const size_t nbase = (size_t)n * OH * OW * C + ch * 8;
         float acc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-        const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(OH - 1, (ih + p) / s);
-        const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(OW - 1, (iw + p) / s);
-        for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-            const int dh = ih - (oh * s - p);
-            if (dh < 0 || dh >= k) continue;
-            for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-                const int dw = iw - (ow * s - p);
-                if (dw < 0 || dw >= k) continue;
-                const int want = dh * k + dw;
-                const size_t off = (((size_t)n * OH + oh) * OW + ow) * C + ch * 8;
-                const u32x4 g = *reinterpret_cast<const u32x4*>(dy + off);
-                const u32x2 ii = *reinterpret_cast<const u32x2*>(idx + off);
+        auto add = [&](const u32x4& g, const u32x2& ii, bool ok, int want) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t w = i < 2 ? ii[0] : ii[1];
-                    const int sh = 16 * (i & 1);
-                    if ((int)((w >> sh) & 0xff) == want) acc[2 * i] += lo_bf(g[i]);
-                    if ((int)((w >> (sh + 8)) & 0xff) == want) acc[2 * i + 1] += hi_bf(g[i]);
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t w = i < 2 ? ii[0] : ii[1];
+                const int sh = 16 * (i & 1);
+                if (ok && (int)((w >> sh) & 0xff) == want) acc[2 * i] += lo_bf(g[i]);
+                if (ok && (int)((w >> (sh + 8)) & 0xff) == want) acc[2 * i + 1] += hi_bf(g[i]);
+            }
+        };
+        // windows containing (ih, iw): oh in [oh_hi - WMAX + 1, oh_hi], oh_hi = (ih + p) / s
+        const int oh_hi = ((int)ih + p) / s, ow_hi = ((int)iw + p) / s;
+        if constexpr (WMAX > 0) {
+            constexpr int WW = WMAX > 0 ? WMAX * WMAX : 1;
+            u32x4 g[WW];
+            u32x2 ii[WW];
+            bool ok[WW];
+            int want[WW];
+#pragma unroll
+            for (int a = 0; a < WMAX; ++a)
+#pragma unroll
+                for (int b = 0; b < WMAX; ++b) {
+                    const int oh = oh_hi - a, ow = ow_hi - b, q = a * WMAX + b;
+                    const int dh = (int)ih - (oh * s - p), dw = (int)iw - (ow * s - p);
+                    ok[q] = oh >= 0 && oh < OH && ow >= 0 && ow < OW && dh < k && dw < k;
+                    want[q] = dh * k + dw;
+                    const size_t off = nbase + ((size_t)min(max(oh, 0), OH - 1) * OW + min(max(ow, 0), OW - 1)) * C;
+                    g[q] = *reinterpret_cast<const u32x4*>(dy + off);
+                    ii[q] = *reinterpret_cast<const u32x2*>(idx + off);
+                }
+#pragma unroll
+            for (int q = 0; q < WMAX * WMAX; ++q) add(g[q], ii[q], ok[q], want[q]);
+        } else {
+            const int oh_lo = max(0, ((int)ih + p - k + s) / s), ow_lo = max(0, ((int)iw + p - k + s) / s);
+            for (int oh = oh_lo; oh <= min(OH - 1, oh_hi); ++oh) {
+                const int dh = (int)ih - (oh * s - p);
+                if (dh < 0 || dh >= k) continue;
+                for (int ow = ow_lo; ow <= min(OW - 1, ow_hi); ++ow) {
+                    const int dw = (int)iw - (ow * s - p);
+                    if (dw < 0 || dw >= k) continue;
+                    const size_t off = nbase + ((size_t)oh * OW + ow) * C;
+                    add(*reinterpret_cast<const u32x4*>(dy + off), *reinterpret_cast<const u32x2*>(idx + off), true,
+                        dh * k + dw);
                 }
             }
         }
         u32x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = pack_bf2(acc[2 * i], acc[2 * i + 1]);
-        *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + ih) * W + iw) * C + ch * 8) = o;
+        *reinterpret_cast<u32x4*>(dx + (size_t)pix * C + ch * 8) = o;
     }
 }
 
@@ -353,9 +402,15 @@ int stream_grid(long work, int per_block = 256) {
 IMK_EXPORT int imk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH,
                                int OW, int k, int s, int p, void* stream) {
     if (C % 8) return -100;
-    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid((long)N * OH * OW * (C / 8))), dim3(256),
-                       0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)idx, N, H, W, C,
-                       OH, OW, k, s, p);
+    const long total = (long)N * OH * OW * (C / 8);
+    if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    const dim3 g(stream_grid(total)), b(256);
+    if (k <= 3)
+        hipLaunchKernelGGL(maxpool_fwd_kernel<3>, g, b, 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
+                           (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p);
+    else
+        hipLaunchKernelGGL(maxpool_fwd_kernel<0>, g, b, 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
+                           (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -363,9 +418,15 @@ IMK_EXPORT int imk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, 
 IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C,
                                int OH, int OW, int k, int s, int p, void* stream) {
     if (C % 8) return -100;
-    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid((long)N * H * W * (C / 8))), dim3(256), 0,
-                       (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, H,
-                       W, C, OH, OW, k, s, p);
+    const long total = (long)N * H * W * (C / 8);
+    if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    const dim3 g(stream_grid(total)), b(256);
+    if ((k + s - 1) / s <= 2)
+        hipLaunchKernelGGL(maxpool_bwd_kernel<2>, g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
+                           (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p);
+    else
+        hipLaunchKernelGGL(maxpool_bwd_kernel<0>, g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
+                           (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p);
     IMK_CHECK_LAUNCH();
     return 0;
 }

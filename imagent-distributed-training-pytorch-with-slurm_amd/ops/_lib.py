@@ -204,6 +204,20 @@ def _declare(name: str, lib) -> None:
         lib.imr_tracker_last_order.restype = i32
         lib.imr_tracker_iterations.argtypes = [vp]
         lib.imr_tracker_iterations.restype = C.c_int64
+        # packed uint8 image records (csrc/runtime/records.cpp, data/records.py)
+        lib.imr_records_header_bytes.restype = i32
+        lib.imr_records_open.argtypes = [C.c_char_p, i32, i32]
+        lib.imr_records_open.restype = vp
+        lib.imr_records_close.argtypes = [vp]
+        lib.imr_records_close.restype = None
+        lib.imr_records_info.argtypes = [vp, vp]
+        lib.imr_records_info.restype = None
+        lib.imr_records_labels.argtypes = [vp, vp]
+        lib.imr_records_labels.restype = None
+        lib.imr_records_submit.argtypes = [vp, i32, vp, i32, vp, vp]
+        lib.imr_records_submit.restype = i32
+        lib.imr_records_wait.argtypes = [vp, i32]
+        lib.imr_records_wait.restype = i32
 
 
 STAT_SLOTS = 32  # conv epilogue statistics slab depth (csrc/kernels/conv_igemm.hip)

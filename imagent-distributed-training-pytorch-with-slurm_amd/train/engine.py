@@ -190,6 +190,18 @@ class Trainer:
             self.n_train, self.n_val = a.synthetic_train_size, a.synthetic_val_size
             self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=a.seed)
             self.val_sampler = ShardSampler(self.n_val, ws, rk, shuffle=True, seed=a.seed)
+        elif a.data == "records":
+            from ..data.records import RecordFile
+            root = a.data_root or os.path.join(os.path.abspath(os.path.join(".", os.pardir)), "data/imagenet")
+            self.train_set = RecordFile(os.path.join(root, "train.imrec"), threads=a.workers)
+            self.val_set = RecordFile(os.path.join(root, "val.imrec"), threads=a.workers)
+            H, W, _ = self.train_set.shape
+            if H < size[0] or W < size[1]:
+                raise SystemExit(f"records hold {H}x{W} images, smaller than --image-size {a.image_size}")
+            self.num_classes = self.train_set.num_classes
+            self.n_train, self.n_val = len(self.train_set), len(self.val_set)
+            self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=0)
+            self.val_sampler = ShardSampler(self.n_val, ws, rk, shuffle=True, seed=0)
         else:
             from ..data.imagenet import ImageNetU8
             root = a.data_root or os.path.join(os.path.abspath(os.path.join(".", os.pardir)), "data/imagenet")
@@ -220,6 +232,12 @@ class Trainer:
             nv = self.val_sampler.num_batches(a.batch_size)
             return (SyntheticLoader(self.train_src, nt, self.transform_train),
                     SyntheticLoader(self.val_src, nv, self.transform_val))
+        if not hasattr(self, "_train_dl") and a.data == "records":
+            from ..data.records import RecordLoader
+            self._train_dl = RecordLoader(self.train_set, self.train_sampler, a.batch_size, self.transform_train,
+                                          self.device)
+            self._val_dl = RecordLoader(self.val_set, self.val_sampler, a.batch_size, self.transform_val,
+                                        self.device)
         if not hasattr(self, "_train_dl"):
             self._train_dl = DeviceLoader(self.train_set, self.train_sampler, a.batch_size,
                                           self.transform_train, self.device, a.workers)

@@ -39,6 +39,21 @@ def test_single_process_two_epochs_and_resume(tmp_path):
     assert "Resumed from" in out2 and "Epoch 3 Summary: " in out2 and "Epoch 1 Summary" not in out2
 
 
+def test_records_data_one_epoch(tmp_path):
+    """--data records: train.imrec / val.imrec through the native gather loader."""
+    import numpy as np
+
+    from imagent_amd.data.records import write_records
+    rng = np.random.default_rng(0)
+    for split, n in (("train", 40), ("val", 12)):
+        imgs = rng.integers(0, 256, (n, 32, 32, 3), dtype=np.uint8)
+        write_records(str(tmp_path / f"{split}.imrec"), zip(imgs, rng.integers(0, 10, n)), n, (32, 32), 10)
+    out = _run(["--arch", "resnet18", "--image-size", "32", "--data", "records", "--data-root", str(tmp_path),
+                "--workers", "2", "--batch-size", "8", "--epochs", "1", "--tb-dir", "", "--quiet-banner"], tmp_path)
+    assert "Training samples: 40 images" in out and "number of classes: 10" in out
+    assert "Epoch 1 Summary: " in out
+
+
 @pytest.mark.slow
 def test_torchrun_two_ranks_gloo(tmp_path):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")

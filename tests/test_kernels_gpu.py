@@ -175,6 +175,64 @@ def test_stem_row_segment_conv():
     assert dw[:, :, :28].reshape(Co, 7, 7, 4)[..., 3].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("shape", [
+    (32, 64, 56, 256, 1, 1, 0),    # K = 64: register-staged persistent grid, two channel panels
+    (32, 256, 14, 1024, 1, 1, 0),  # K = 256: 256x256 LDS-DMA persistent grid, four panels
+    (128, 256, 28, 64, 1, 1, 0),   # Nout = 64: one panel per block for its whole life
+])
+def test_conv_stats_persistent_blocks(shape):
+    """Short-K convs run on a persistent grid (blocks walk many tiles) and carry
+    their BN statistics in registers across a channel panel: the slab must
+    still hold exactly the sums of the stored bf16 output."""
+    from imagent_amd.ops.conv import igemm_fwd
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(4)
+    x = bf(torch.randn(N, H, H, Ci, device=DEV))
+    w = bf(torch.randn(Co, k, k, Ci, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5)
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(x, w, s, p, k, k, stats=slab)
+    ref = F.conv2d(nchw(x).float(), nchw(w).float(), None, s, p)
+    assert rel(nchw(y), ref) < 1e-2
+    yb = y.float().reshape(-1, Co)
+    st = slab.sum(0)
+    assert rel(st[0], yb.sum(0)) < 1e-4
+    assert rel(st[1], (yb * yb).sum(0)) < 1e-4
+
+
+def test_stem_stats_persistent_blocks():
+    """Full-size stem (224^2 -> 112^2, 16 images): persistent grid, one channel panel."""
+    from imagent_amd.ops.conv import igemm_fwd
+    torch.manual_seed(8)
+    N, H, Co = 16, 224, 64
+    x4 = torch.zeros(N, H, H, 4, device=DEV, dtype=torch.bfloat16)
+    x4[..., :3] = bf(torch.randn(N, H, H, 3, device=DEV))
+    wrow = torch.zeros(Co, 7, 32, device=DEV, dtype=torch.bfloat16)
+    w3 = bf(torch.randn(Co, 3, 7, 7, device=DEV) * 0.1)
+    wrow[:, :, :28].view(Co, 7, 7, 4)[..., :3] = w3.permute(0, 2, 3, 1)
+    slab = torch.zeros(32, 2, Co, device=DEV)
+    y = igemm_fwd(x4, wrow, 2, 3, 7, 7, stats=slab, stem=True)
+    ref = F.conv2d(nchw(x4[..., :3]).float(), w3.float(), None, 2, 3)
+    assert rel(nchw(y), ref) < 1e-2
+    yb = y.float().reshape(-1, Co)
+    assert rel(slab.sum(0)[0], yb.sum(0)) < 1e-4
+    assert rel(slab.sum(0)[1], (yb * yb).sum(0)) < 1e-4
+
+
+def test_maxpool_stem_size():
+    """The stem's pool at a full-size row (112 px, 64 ch): row-grid indexing."""
+    from imagent_amd.ops.misc import MaxPoolFn
+    torch.manual_seed(5)
+    x = bf(torch.randn(3, 112, 112, 64, device=DEV)).requires_grad_(True)
+    y = MaxPoolFn.apply(x, 3, 2, 1)
+    xr = nchw(x.detach()).float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(nchw(y).float(), yr)
+    g = bf(torch.randn_like(y))
+    y.backward(g)
+    yr.backward(nchw(g).float())
+    assert rel(nchw(x.grad), xr.grad) < 1e-2
+
+
 def test_conv_fwd_bias_fp32_out():
     from imagent_amd.ops.conv import igemm_fwd
     torch.manual_seed(1)
