@@ -20,7 +20,16 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     const int md = (a.C % BK) == 0 ? 0 : 1;
+    // short-K 1x1 convs (K = C = 64 / 128) are HBM streams: weights resident in
+    // LDS, pixel fragments straight from HBM (conv_stream.hip); tiles 20/21/22
+    // force its 256/128/64-channel slices (A/B testing)
+    const int bn_hint = tile >= 20 ? 256 >> (tile - 20) : 0;
+    if (tile >= 20) tile = 0;
     const bool autotile = tile == 0;
+    if (autotile && a.nth == 1 && a.ntw == 1 && (a.C == 64 || a.C == 128)) {
+        const int r = conv_stream(a, st, bn_hint);
+        if (r != 1) return r;
+    }
     if (autotile) tile = (a.Nout <= 64) ? 4 : 2;
     // measured on MI355X (profiles/r50_conv_layers_*): the register-staged
     // pipeline wins for 64-wide output tiles and single-stage (K <= 64) tiles,

@@ -93,6 +93,7 @@ struct IGemmArgs {
 #define IG_FP8 256     // fp8 operands on the block-scaled MFMA (conv_igemm_fp8.hip)
 #define IG_BF8X 512    // with IG_FP8: the gathered operand X is e5m2 (gradients), Wk e4m3
 #define IG_AFFINE 1024 // inference BN folded into the epilogue: out = acc * bias[n] + bias[Nout + n]
+#define IG_NOSTREAM 2048  // never the streaming short-K 1x1 kernel (conv_stream.hip; A/B testing)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 static __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes (per TU)
@@ -987,3 +988,6 @@ int launch_rs(const IGemmArgs& a, hipStream_t st) {
 // fp8 paths live in their own translation unit (conv_igemm_fp8.hip) so the
 // two halves of the kernel set compile in parallel
 int conv_igemm_fp8(const IGemmArgs& a, int tile, hipStream_t st);
+// short-K (C in {64, 128}) 1x1 convolutions as an HBM stream (conv_stream.hip);
+// returns 1 when the shape / flags are not covered
+int conv_stream(const IGemmArgs& a, hipStream_t st, int bn = 0);

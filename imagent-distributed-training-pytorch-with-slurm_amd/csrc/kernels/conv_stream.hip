@@ -1,0 +1,308 @@
+// Streaming 1x1 convolution for SHORT reductions (K = C in {64, 128}), gfx950.
+//
+// ResNet bottlenecks spend their 56x56 / 28x28 stages in 1x1 convolutions with
+// K = 64 or 128: the expansion conv3 (64 -> 256, 128 -> 512) forward, and the
+// dgrad of conv1 (256 -> 64, 512 -> 128: dX[M][256] = dY[M][64] x W) with the
+// BN-backward epilogue. These are pure HBM streams (output bytes = 4x input
+// bytes) -- the generic tiled kernels (conv_igemm_impl.h) reload the weight
+// tile per output tile, keep one 16-KB stage in flight per block and measured
+// 2.1 TB/s on them (profiles/r50_b512_v5_*). Same jobs as cuDNN's conv fwd /
+// dgrad for those shapes (reference model imagenet.py:312).
+//
+// Structure (one persistent block = 4 waves per (pixel range, channel slice)):
+//  * the block's weight slice [BN][K] lives in LDS for the whole kernel
+//    (16-B chunks XOR-swizzled by row -> conflict-free ds_read_b128 A
+//    fragments);
+//  * each wave walks 16-pixel groups; the pixel operand is the MFMA B
+//    fragment, and in NHWC one lane's B fragment (8 consecutive channels of
+//    one pixel) is ONE 16-B global load -- no LDS staging at all. D groups
+//    are prefetched into registers ahead of use (bytes in flight per CU ~
+//    8 waves x D x 2-4 KB);
+//  * v_mfma_f32_16x16x32_bf16, weights = A (rows = output channels);
+//  * epilogue per group: the 16 x BN bf16 tile goes through a wave-private LDS
+//    buffer and comes back as 16-B row chunks, so every global store / read of
+//    the epilogue is a coalesced row segment, and each lane always holds the
+//    SAME 8 channels -> BatchNorm statistics (forward: sum, sumsq; IG_BNBWD:
+//    sum(g*xhat), sum(g) [, sum(g*xhat2)]) accumulate in 16-24 registers over
+//    the whole kernel and leave with one lane fold + one atomic per channel
+//    and quantity per wave.
+// Semantics are those of igemm's plain / IG_ACCUM / IG_BNBWD epilogues.
+
+#include "conv_igemm_impl.h"
+
+namespace {
+
+template <int K, int BN, int D, bool BNB>  // BNB: IG_BNBWD epilogue (else plain, optional IG_ACCUM)
+__global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) {
+    constexpr int KS = K / 32;        // MFMA k-steps per group
+    constexpr int FN = BN / 16;       // channel fragments
+    constexpr int CPR = K / 8;        // 16-B chunks per weight row
+    constexpr int EP = BN * 2 + 16;   // epilogue LDS row pitch (bytes)
+    constexpr int CH = BN / 8;        // 16-B output chunks per pixel
+    constexpr int PPR = 64 / CH;      // pixels per epilogue read instruction
+    constexpr int NR = 16 / PPR;      // epilogue reads per 16-pixel group
+    constexpr int QBM = BNB ? 2 : 4;
+    constexpr int QB = NR < QBM ? NR : QBM;  // chunks whose global reads are batched
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    char* sW = smem;
+    char* sE = smem + BN * K * 2 + wid * 16 * EP;
+
+    const int nsl = a.Nout / BN;
+    const int G = gridDim.x;  // multiple of nsl (host)
+    const int lid = xcd_remap(blockIdx.x, G);
+    const int slice = lid % nsl, pb = lid / nsl, npb = G / nsl;
+    const int n0 = slice * BN;
+    const bool accum = a.flags & IG_ACCUM;
+    constexpr bool bnb = BNB;
+    const bool has_y = bnb && a.bny, has_x2 = bnb && a.bnx2;
+
+    // weight slice -> LDS: chunk c of row r at slot c ^ (r % CPR)
+    for (int idx = tid; idx < BN * CPR; idx += 256) {
+        const int r = idx / CPR, c = idx % CPR;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(a.Wk + (size_t)(n0 + r) * a.ldb + c * 8);
+        *reinterpret_cast<u32x4*>(sW + r * K * 2 + ((c ^ (r % CPR)) * 16)) = v;
+    }
+
+    // fixed epilogue channel chunk of this lane + the BN constants it needs
+    const int cc = lane % CH;
+    const int n = n0 + cc * 8;
+    float mean[8], rstd[8], sc[8], sh[8], m2[8], r2[8];
+    if (bnb) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 mu = *reinterpret_cast<const f32x4*>(a.bnsave + n + 4 * h);
+            const f32x4 rs = *reinterpret_cast<const f32x4*>(a.bnsave + a.Nout + n + 4 * h);
+            f32x4 g = {0.f, 0.f, 0.f, 0.f}, b = g, mu2 = g, rs2 = g;
+            if (!has_y) {
+                g = *reinterpret_cast<const f32x4*>(a.bngamma + n + 4 * h);
+                b = *reinterpret_cast<const f32x4*>(a.bnbeta + n + 4 * h);
+            }
+            if (has_x2) {
+                mu2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + n + 4 * h);
+                rs2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + a.Nout + n + 4 * h);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                mean[4 * h + r] = mu[r];
+                rstd[4 * h + r] = rs[r];
+                sc[4 * h + r] = g[r] * rs[r];
+                sh[4 * h + r] = b[r] - mu[r] * sc[4 * h + r];
+                m2[4 * h + r] = mu2[r];
+                r2[4 * h + r] = rs2[r];
+            }
+        }
+    }
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
+
+    const int ohw = a.OH * a.OW;
+    const bool dense = a.sA == 1 && a.H == a.OH && a.W == a.OW;  // input row == output pixel
+    const int ngroups = (a.M + 15) / 16;
+    const int wstride = npb * 4;
+    const int w0 = pb * 4 + wid;
+    const int fr = lane & 15, fq = lane >> 4;
+
+    u32x4 pf[D][KS];
+    auto fetch = [&](int d, int g) {
+        const int m = g * 16 + fr;
+        const bool ok = g < ngroups && m < a.M;
+        size_t row = 0;
+        if (ok) {
+            if (dense) {
+                row = (size_t)m;
+            } else {
+                const int img = m / ohw, rem = m - img * ohw;
+                const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                row = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
+            }
+        }
+        const bf16_t* p = a.X + row * a.C + fq * 8;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(p + ks * 32) : u32x4{0u, 0u, 0u, 0u};
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) fetch(d, w0 + d * wstride);
+    __syncthreads();  // weight slice visible
+
+    int aoff[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * K * 2 + (((ks * 4 + fq) ^ (fr % CPR)) * 16);
+
+    for (int g0 = w0; g0 < ngroups; g0 += D * wstride) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int g = g0 + d * wstride;
+            if (g >= ngroups) break;
+            bf16x8 fb[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) fb[ks] = __builtin_bit_cast(bf16x8, pf[d][ks]);
+            fetch(d, g + D * wstride);
+            f32x4 acc[FN];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int i = 0; i < FN; ++i) {
+                    const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sW + i * 16 * K * 2 + aoff[ks]);
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[ks], acc[i], 0, 0, 0);
+                }
+            // (1) fragments -> wave-private LDS rows (pixel fr, 4 channels per lane).
+            // DS instructions of one wave execute in order: the re-reads below see
+            // these writes, and the previous group's reads are complete (their
+            // results were consumed) before these writes land.
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+                *reinterpret_cast<u32x2*>(sE + fr * EP + (i * 16 + fq * 4) * 2) =
+                    u32x2{pack_bf2(acc[i][0], acc[i][1]), pack_bf2(acc[i][2], acc[i][3])};
+            __builtin_amdgcn_wave_barrier();
+            // (2) coalesced row chunks: pixel q*PPR + lane/CH, channels n .. n+7
+#pragma unroll
+            for (int q0 = 0; q0 < NR; q0 += QB) {
+                long e[QB];
+                u32x4 oo[QB], xo[QB], yo[QB], x2o[QB];
+#pragma unroll
+                for (int u = 0; u < QB; ++u) {
+                    const int m = g * 16 + (q0 + u) * PPR + lane / CH;
+                    e[u] = m < a.M ? (long)m * a.ldy + n : -1;
+                    if (e[u] >= 0) {
+                        if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
+                        if (bnb) {
+                            xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                            if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
+                            if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < QB; ++u) {
+                    const int p = (q0 + u) * PPR + lane / CH;
+                    const u32x4 t = *reinterpret_cast<const u32x4*>(sE + p * EP + cc * 16);
+                    if (e[u] < 0) continue;
+                    float v[8];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        v[2 * k] = lo_bf(t[k]);
+                        v[2 * k + 1] = hi_bf(t[k]);
+                        if (accum) {
+                            v[2 * k] += lo_bf(oo[u][k]);
+                            v[2 * k + 1] += hi_bf(oo[u][k]);
+                        }
+                    }
+                    float xv[8];
+                    if (bnb) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            xv[2 * k] = lo_bf(xo[u][k]);
+                            xv[2 * k + 1] = hi_bf(xo[u][k]);
+                        }
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) {
+                            const bool keep = has_y ? ((c & 1 ? hi_bf(yo[u][c >> 1]) : lo_bf(yo[u][c >> 1])) > 0.f)
+                                                    : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
+                            if (!keep) v[c] = 0.f;
+                        }
+                    }
+                    u32x4 o;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+                    *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[u]) = o;
+                    if (a.stats) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {  // statistics of the stored (bf16) values
+                            v[2 * k] = lo_bf(o[k]);
+                            v[2 * k + 1] = hi_bf(o[k]);
+                        }
+                        if (bnb) {
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) {
+                                s1[c] += v[c] * ((xv[c] - mean[c]) * rstd[c]);
+                                s2[c] += v[c];
+                            }
+                            if (has_x2) {
+#pragma unroll
+                                for (int c = 0; c < 8; ++c) {
+                                    const float x2 = c & 1 ? hi_bf(x2o[u][c >> 1]) : lo_bf(x2o[u][c >> 1]);
+                                    s3[c] += v[c] * ((x2 - m2[c]) * r2[c]);
+                                }
+                            }
+                        } else {
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) {
+                                s1[c] += v[c];
+                                s2[c] += v[c] * v[c];
+                            }
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (!a.stats) return;
+    // fold the lanes that share a channel chunk, one atomic per channel and quantity
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int o = CH; o < 64; o <<= 1) {
+            s1[c] += __shfl_xor(s1[c], o, 64);
+            s2[c] += __shfl_xor(s2[c], o, 64);
+            if (has_x2) s3[c] += __shfl_xor(s3[c], o, 64);
+        }
+    }
+    if (lane >= CH) return;
+    float* st = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * (bnb ? 3 : 2) * a.Nout;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        atomicAdd(st + n + c, s1[c]);
+        atomicAdd(st + a.Nout + n + c, s2[c]);
+        if (has_x2) atomicAdd(st + 2 * a.Nout + n + c, s3[c]);
+    }
+}
+
+template <int K, int BN, int D, bool BNB>
+int launch_stream1(const IGemmArgs& a, hipStream_t st) {
+    const size_t lds = (size_t)BN * K * 2 + 4 * 16 * (BN * 2 + 16);
+    static int resident = 0;
+    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, BNB>, lds);
+    const int nsl = a.Nout / BN;
+    const int ngroups = (a.M + 15) / 16;
+    // enough pixel blocks to fill the chip, but >= D groups per wave
+    const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
+    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, BNB>), dim3(npb * nsl), dim3(256), lds, st, a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+template <int K, int BN, int D>
+int launch_stream(const IGemmArgs& a, hipStream_t st) {
+    return (a.flags & IG_BNBWD) ? launch_stream1<K, BN, D, true>(a, st) : launch_stream1<K, BN, D, false>(a, st);
+}
+
+}  // namespace
+
+// Returns 1 if the shape is not one this kernel covers (caller falls back).
+// bn: channel-slice width (0 auto: the widest that divides Nout; 64/128/256 forced)
+int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
+    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
+    if (a.bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
+    if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
+    if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
+    if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
+    const int maxbn = a.C == 64 ? 256 : 128;
+    if (bn == 0) bn = maxbn;
+    while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
+    if (a.C == 64) {
+        if (bn == 256) return launch_stream<64, 256, 3>(a, st);
+        if (bn == 128) return launch_stream<64, 128, 3>(a, st);
+        return launch_stream<64, 64, 3>(a, st);
+    }
+    if (a.C == 128) {
+        if (bn == 128) return launch_stream<128, 128, 2>(a, st);
+        return launch_stream<128, 64, 2>(a, st);
+    }
+    return 1;
+}

@@ -13,6 +13,7 @@ Reference counterpart: the cuDNN convolutions torchvision's resnet issues
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -48,6 +49,15 @@ def _base_args(x_ptr, w_ptr, y_ptr, N, H, W, Cin, OH, OW, Nout, ldb, sA) -> _lib
 # epilogue choice: 0 auto (LDS-staged for fused BN backward, else direct),
 # 1 direct register epilogue, 2 LDS-staged coalesced epilogue
 _EPI_FLAGS = {0: 0, 1: 128, 2: 64}
+# IMAGENT_CONV_STREAM=0: keep short-K 1x1 convs off the streaming kernel
+# (conv_stream.hip) -- A/B switch for benchmarks and numerics tests
+_NOSTREAM = 2048 if os.environ.get("IMAGENT_CONV_STREAM", "1") == "0" else 0
+
+
+def set_stream(enabled: bool) -> None:
+    """Route short-K (C in {64, 128}) 1x1 convs to the streaming kernel or not."""
+    global _NOSTREAM
+    _NOSTREAM = 0 if enabled else 2048
 
 
 def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
@@ -80,7 +90,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
     a.flags = (1 if out_f32 else 0) | (2 if relu else 0) | (4 if stem else 0) | _EPI_FLAGS[epi] | \
-        (8 if accumulate else 0)
+        (8 if accumulate else 0) | _NOSTREAM
     if affine is not None:
         assert bias is None and affine.shape == (2, Co) and affine.dtype == torch.float32
         a.flags |= 1024
@@ -156,7 +166,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi] | (256 | 512 if fp8 is not None else 0)
+            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi] | (256 | 512 if fp8 is not None else 0) | _NOSTREAM
             if bnb is not None:
                 bnb.fill(a)
             _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")
