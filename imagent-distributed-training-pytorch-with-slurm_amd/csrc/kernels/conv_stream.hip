@@ -32,7 +32,9 @@
 
 namespace {
 
-template <int K, int BN, int D, bool BNB>  // BNB: IG_BNBWD epilogue (else plain, optional IG_ACCUM)
+// MODE 0: plain epilogue (+ optional IG_ACCUM); IG_BNBWD with the ReLU mask
+// from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3)
+template <int K, int BN, int D, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) {
     constexpr int KS = K / 32;        // MFMA k-steps per group
     constexpr int FN = BN / 16;       // channel fragments
@@ -41,8 +43,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     constexpr int CH = BN / 8;        // 16-B output chunks per pixel
     constexpr int PPR = 64 / CH;      // pixels per epilogue read instruction
     constexpr int NR = 16 / PPR;      // epilogue reads per 16-pixel group
-    constexpr int QBM = BNB ? 2 : 4;
-    constexpr int QB = NR < QBM ? NR : QBM;  // chunks whose global reads are batched
+    constexpr bool bnb = MODE != 0, has_y = MODE == 1 || MODE == 3, has_x2 = MODE == 3;
+    // chunks whose global reads are batched; with the BN-backward epilogue all
+    // of a group's reads (x, y | x2, old) are issued before its MFMAs
+    constexpr int QB = bnb ? NR : (NR < 4 ? NR : 4);
+    static_assert(!bnb || NR <= 4, "BN-backward epilogue: slices of <= 128 channels");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     char* sW = smem;
@@ -54,8 +59,6 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     const int slice = lid % nsl, pb = lid / nsl, npb = G / nsl;
     const int n0 = slice * BN;
     const bool accum = a.flags & IG_ACCUM;
-    constexpr bool bnb = BNB;
-    const bool has_y = bnb && a.bny, has_x2 = bnb && a.bnx2;
 
     // weight slice -> LDS: chunk c of row r at slot c ^ (r % CPR)
     for (int idx = tid; idx < BN * CPR; idx += 256) {
@@ -140,6 +143,24 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) fb[ks] = __builtin_bit_cast(bf16x8, pf[d][ks]);
             fetch(d, g + D * wstride);
+            long e[NR];
+            u32x4 oo[NR], xo[NR], yo[NR], x2o[NR];
+            auto issue = [&](int u) {
+                const int m = g * 16 + u * PPR + lane / CH;
+                e[u] = m < a.M ? (long)m * a.ldy + n : -1;
+                if (e[u] >= 0) {
+                    if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
+                    if (bnb) {
+                        xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                        if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
+                        if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
+                    }
+                }
+            };
+            if (bnb) {
+#pragma unroll
+                for (int u = 0; u < NR; ++u) issue(u);
+            }
             f32x4 acc[FN];
 #pragma unroll
             for (int i = 0; i < FN; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -162,46 +183,36 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             // (2) coalesced row chunks: pixel q*PPR + lane/CH, channels n .. n+7
 #pragma unroll
             for (int q0 = 0; q0 < NR; q0 += QB) {
-                long e[QB];
-                u32x4 oo[QB], xo[QB], yo[QB], x2o[QB];
+                if (!bnb) {
 #pragma unroll
-                for (int u = 0; u < QB; ++u) {
-                    const int m = g * 16 + (q0 + u) * PPR + lane / CH;
-                    e[u] = m < a.M ? (long)m * a.ldy + n : -1;
-                    if (e[u] >= 0) {
-                        if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
-                        if (bnb) {
-                            xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
-                            if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
-                            if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
-                        }
-                    }
+                    for (int u = 0; u < QB; ++u) issue(q0 + u);
                 }
 #pragma unroll
                 for (int u = 0; u < QB; ++u) {
-                    const int p = (q0 + u) * PPR + lane / CH;
+                    const int q = q0 + u;
+                    const int p = q * PPR + lane / CH;
                     const u32x4 t = *reinterpret_cast<const u32x4*>(sE + p * EP + cc * 16);
-                    if (e[u] < 0) continue;
+                    if (e[q] < 0) continue;
                     float v[8];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         v[2 * k] = lo_bf(t[k]);
                         v[2 * k + 1] = hi_bf(t[k]);
                         if (accum) {
-                            v[2 * k] += lo_bf(oo[u][k]);
-                            v[2 * k + 1] += hi_bf(oo[u][k]);
+                            v[2 * k] += lo_bf(oo[q][k]);
+                            v[2 * k + 1] += hi_bf(oo[q][k]);
                         }
                     }
                     float xv[8];
                     if (bnb) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            xv[2 * k] = lo_bf(xo[u][k]);
-                            xv[2 * k + 1] = hi_bf(xo[u][k]);
+                            xv[2 * k] = lo_bf(xo[q][k]);
+                            xv[2 * k + 1] = hi_bf(xo[q][k]);
                         }
 #pragma unroll
                         for (int c = 0; c < 8; ++c) {
-                            const bool keep = has_y ? ((c & 1 ? hi_bf(yo[u][c >> 1]) : lo_bf(yo[u][c >> 1])) > 0.f)
+                            const bool keep = has_y ? ((c & 1 ? hi_bf(yo[q][c >> 1]) : lo_bf(yo[q][c >> 1])) > 0.f)
                                                     : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
                             if (!keep) v[c] = 0.f;
                         }
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     u32x4 o;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
-                    *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[u]) = o;
+                    *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[q]) = o;
                     if (a.stats) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {  // statistics of the stored (bf16) values
@@ -225,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             if (has_x2) {
 #pragma unroll
                                 for (int c = 0; c < 8; ++c) {
-                                    const float x2 = c & 1 ? hi_bf(x2o[u][c >> 1]) : lo_bf(x2o[u][c >> 1]);
+                                    const float x2 = c & 1 ? hi_bf(x2o[q][c >> 1]) : lo_bf(x2o[q][c >> 1]);
                                     s3[c] += v[c] * ((x2 - m2[c]) * r2[c]);
                                 }
                             }
@@ -263,23 +274,28 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     }
 }
 
-template <int K, int BN, int D, bool BNB>
+template <int K, int BN, int D, int MODE>
 int launch_stream1(const IGemmArgs& a, hipStream_t st) {
     const size_t lds = (size_t)BN * K * 2 + 4 * 16 * (BN * 2 + 16);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, BNB>, lds);
+    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE>, lds);
     const int nsl = a.Nout / BN;
     const int ngroups = (a.M + 15) / 16;
     // enough pixel blocks to fill the chip, but >= D groups per wave
     const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
-    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, BNB>), dim3(npb * nsl), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE>), dim3(npb * nsl), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
 template <int K, int BN, int D>
 int launch_stream(const IGemmArgs& a, hipStream_t st) {
-    return (a.flags & IG_BNBWD) ? launch_stream1<K, BN, D, true>(a, st) : launch_stream1<K, BN, D, false>(a, st);
+    if (!(a.flags & IG_BNBWD)) return launch_stream1<K, BN, D, 0>(a, st);
+    if constexpr (BN <= 128) {
+        if (a.bnx2) return a.bny ? launch_stream1<K, BN, D, 3>(a, st) : 1;
+        return a.bny ? launch_stream1<K, BN, D, 1>(a, st) : launch_stream1<K, BN, D, 2>(a, st);
+    }
+    return 1;
 }
 
 }  // namespace
@@ -292,7 +308,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
-    const int maxbn = a.C == 64 ? 256 : 128;
+    const int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (bn == 0) bn = maxbn;
     while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
     if (a.C == 64) {
