@@ -28,6 +28,8 @@
 //    and quantity per wave.
 // Semantics are those of igemm's plain / IG_ACCUM / IG_BNBWD epilogues.
 
+#include <cstdlib>
+
 #include "conv_igemm_impl.h"
 
 namespace {
@@ -308,7 +310,16 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
-    const int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
+    int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
+    if (a.flags & IG_BNBWD) {
+        // BN-backward epilogue: IMAGENT_STREAM_BNB = 0 (never), 64 / 128 (slice width)
+        static const int pref = [] {
+            const char* e = getenv("IMAGENT_STREAM_BNB");
+            return e ? atoi(e) : 64;
+        }();
+        if (pref == 0) return 1;
+        maxbn = pref >= 128 ? 128 : 64;
+    }
     if (bn == 0) bn = maxbn;
     while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
     if (a.C == 64) {

@@ -22,6 +22,8 @@
 // chip-wide atomic rate, ~1.3 TB/s, is far above what these tiles need).
 // Index math for the gather uses host-computed magic-number division.
 
+#include <cstdlib>
+
 #include "common.h"
 
 struct WgradArgs {
@@ -38,7 +40,6 @@ struct WgradArgs {
 
 namespace {
 
-constexpr int BR = 64;  // pixels (reduction rows) per stage
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
     return (uint32_t)(((uint64_t)__umulhi(n, mg) + n) >> sh);
@@ -46,8 +47,10 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
 
 // NW waves per block: 4 (two blocks per CU) or 8 (one 256x256 block per CU:
 // half the operand bytes per MFMA FLOP of a 128x128 tile)
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void wgrad_kernel(const WgradArgs a) {
+// BR: pixels (reduction rows) per stage -- 64, or 32 (half the LDS: three
+// 4-wave blocks per CU instead of two, more waves to hide the load latency)
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgrad_kernel(const WgradArgs a) {
     constexpr int NT = NW * 64;
     constexpr int WKC = NW / WCO;
     constexpr int TCO = BCO / WCO, TKC = BKC / WKC;
@@ -220,8 +223,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void wgrad_kernel(const W
         }
 }
 
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4>
-int launch(WgradArgs a, int splits, hipStream_t st) {
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64>
+int launch1(WgradArgs a, int splits, hipStream_t st) {
     const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
     if (splits <= 0) {
@@ -237,9 +240,24 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
-    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW>), dim3(ntiles * splits), dim3(NW * 64), lds, st, a);
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR>), dim3(ntiles * splits), dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
+}
+
+// Stage depth by shape (measured, 1x MI355X, R50 @ 512 img): 32-row stages win
+// on 1x1 convs, the stem and 64-channel tiles (-8..-20 %), 64-row stages on
+// the 3x3 convs with 128x128 tiles (-15..-25 % vs 32). IMAGENT_WGRAD_BR=32|64
+// forces one.
+template <int BCO, int BKC, int WCO, bool STEM>
+int launch(WgradArgs a, int splits, hipStream_t st) {
+    static const int force = [] {
+        const char* e = getenv("IMAGENT_WGRAD_BR");
+        return e ? atoi(e) : 0;
+    }();
+    const bool br32 = force ? force == 32 : (STEM || BCO == 64 || a.KH * a.KW == 1);
+    return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32>(a, splits, st)
+                : launch1<BCO, BKC, WCO, STEM, 4, 64>(a, splits, st);
 }
 
 }  // namespace
