@@ -36,11 +36,18 @@ namespace {
 
 // MODE 0: plain epilogue (+ optional IG_ACCUM); IG_BNBWD with the ReLU mask
 // from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3)
-template <int K, int BN, int D, int MODE>
+// STEM: the 7x7/2 stem as a row-segment gather (C = 4 padded channels, a
+// kernel row = 8 taps x 4 channels = 32 K elements, K = KH x 32): one MFMA
+// k-step per kernel row, the lane's B fragment = 2 taps x 4 channels = two
+// 8-B loads (each predicated on the image border).
+template <int K, int BN, int D, int MODE, bool STEM = false>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) {
     constexpr int KS = K / 32;        // MFMA k-steps per group
     constexpr int FN = BN / 16;       // channel fragments
     constexpr int CPR = K / 8;        // 16-B chunks per weight row
+    constexpr int RP = STEM ? 32 : CPR;             // LDS weight row pitch, chunks (power of two)
+    constexpr int RB = RP * 16;                     // ... bytes
+    constexpr int SWM = (RP < 16 ? RP : 16) - 1;    // chunk swizzle mask: conflict-free A reads
     constexpr int EP = BN * 2 + 16;   // epilogue LDS row pitch (bytes)
     constexpr int CH = BN / 8;        // 16-B output chunks per pixel
     constexpr int PPR = 64 / CH;      // pixels per epilogue read instruction
@@ -53,7 +60,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     char* sW = smem;
-    char* sE = smem + BN * K * 2 + wid * 16 * EP;
+    char* sE = smem + BN * RB + wid * 16 * EP;
 
     const int nsl = a.Nout / BN;
     const int G = gridDim.x;  // multiple of nsl (host)
@@ -62,11 +69,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     const int n0 = slice * BN;
     const bool accum = a.flags & IG_ACCUM;
 
-    // weight slice -> LDS: chunk c of row r at slot c ^ (r % CPR)
+    // weight slice -> LDS: chunk c of row r at slot c ^ (r & SWM)
     for (int idx = tid; idx < BN * CPR; idx += 256) {
         const int r = idx / CPR, c = idx % CPR;
         const u32x4 v = *reinterpret_cast<const u32x4*>(a.Wk + (size_t)(n0 + r) * a.ldb + c * 8);
-        *reinterpret_cast<u32x4*>(sW + r * K * 2 + ((c ^ (r % CPR)) * 16)) = v;
+        *reinterpret_cast<u32x4*>(sW + r * RB + ((c ^ (r & SWM)) * 16)) = v;
     }
 
     // fixed epilogue channel chunk of this lane + the BN constants it needs
@@ -113,6 +120,31 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     auto fetch = [&](int d, int g) {
         const int m = g * 16 + fr;
         const bool ok = g < ngroups && m < a.M;
+        if constexpr (STEM) {
+            int img = 0, oh = 0, ow = 0;
+            if (ok) {
+                img = m / ohw;
+                const int rem = m - img * ohw;
+                oh = rem / a.OW;
+                ow = rem - oh * a.OW;
+            }
+            const int kw0 = 2 * fq;
+            const int iw = ow * a.sA + a.dw0 + kw0;
+            const bool lo_w = ok && kw0 < a.ntw && (unsigned)iw < (unsigned)a.W;
+            const bool hi_w = ok && kw0 + 1 < a.ntw && (unsigned)(iw + 1) < (unsigned)a.W;
+            const bf16_t* base = a.X + (size_t)img * a.H * a.W * 4;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int ih = oh * a.sA + a.dh0 + ks;
+                const bool rok = ks < a.nth && (unsigned)ih < (unsigned)a.H;
+                const bf16_t* q = base + ((long)ih * a.W + iw) * 4;
+                u32x2 lo = {0u, 0u}, hi = {0u, 0u};
+                if (rok && lo_w) lo = *reinterpret_cast<const u32x2*>(q);
+                if (rok && hi_w) hi = *reinterpret_cast<const u32x2*>(q + 4);
+                pf[d][ks] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+            }
+            return;
+        }
         size_t row = 0;
         if (ok) {
             if (dense) {
@@ -134,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
 
     int aoff[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * K * 2 + (((ks * 4 + fq) ^ (fr % CPR)) * 16);
+    for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((ks * 4 + fq) ^ (fr & SWM)) * 16);
 
     for (int g0 = w0; g0 < ngroups; g0 += D * wstride) {
 #pragma unroll
@@ -170,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
                 for (int i = 0; i < FN; ++i) {
-                    const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sW + i * 16 * K * 2 + aoff[ks]);
+                    const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sW + i * 16 * RB + aoff[ks]);
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[ks], acc[i], 0, 0, 0);
                 }
             // (1) fragments -> wave-private LDS rows (pixel fr, 4 channels per lane).
@@ -276,16 +308,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     }
 }
 
-template <int K, int BN, int D, int MODE>
+template <int K, int BN, int D, int MODE, bool STEM = false>
 int launch_stream1(const IGemmArgs& a, hipStream_t st) {
-    const size_t lds = (size_t)BN * K * 2 + 4 * 16 * (BN * 2 + 16);
+    constexpr int RP = STEM ? 32 : K / 8;
+    const size_t lds = (size_t)BN * RP * 16 + 4 * 16 * (BN * 2 + 16);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE>, lds);
+    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM>, lds);
     const int nsl = a.Nout / BN;
     const int ngroups = (a.M + 15) / 16;
     // enough pixel blocks to fill the chip, but >= D groups per wave
     const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
-    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE>), dim3(npb * nsl), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM>), dim3(npb * nsl), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -305,7 +338,14 @@ int launch_stream(const IGemmArgs& a, hipStream_t st) {
 // Returns 1 if the shape is not one this kernel covers (caller falls back).
 // bn: channel-slice width (0 auto: the widest that divides Nout; 64/128/256 forced)
 int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
-    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
+    if (a.flags & IG_STEM) {  // 7x7 stem, C = 4, K = 7 x 32
+        if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_ACCUM | IG_BNBWD | IG_NOSTREAM)) return 1;
+        if (a.bias || a.C != 4 || a.nth != 7 || a.ntw > 8 || a.ldb != 7 * 32 || a.Nout % 64 || a.ldy != a.Nout ||
+            a.sY != 1 || a.YH != a.OH || a.YW != a.OW)
+            return 1;
+        return launch_stream1<7 * 32, 64, 2, 0, true>(a, st);
+    }
+    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
     if (a.bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
@@ -315,7 +355,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         // BN-backward epilogue: IMAGENT_STREAM_BNB = 0 (never), 64 / 128 (slice width)
         static const int pref = [] {
             const char* e = getenv("IMAGENT_STREAM_BNB");
-            return e ? atoi(e) : 64;
+            return e ? atoi(e) : 128;
         }();
         if (pref == 0) return 1;
         maxbn = pref >= 128 ? 128 : 64;
