@@ -97,15 +97,42 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
     }
 }
 
+// Optional BatchNorm-backward epilogue for the stem (BNR): the pool's input
+// gradient g is the upstream gradient of BN+ReLU(x); the kernel stores it
+// ReLU-masked (mask recomputed from x) and reduces sum(g*xhat), sum(g) per
+// channel into slot (block & 31) of the BN's [32][3][C] backward slab -- the
+// separate reduce pass over (g, x) disappears (bn.hip bn_bwd_reduce_kernel).
+struct PoolBnr {
+    const bf16_t* x;     // BN input, NHWC like dx
+    const float* save;   // [2][C] mean, rstd
+    const float* gamma;
+    const float* beta;
+    float* slab;         // [32][3][C]
+};
+
 // WMAX > 0: at most WMAX candidate windows per dimension (ceil(k/s) <= WMAX),
 // unrolled; 0: generic
-template <int WMAX>
+template <int WMAX, bool BNR = false>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           bf16_t* __restrict__ dx, int N, int H, int W,
-                                                          int C, int OH, int OW, int k, int s, int p) {
+                                                          int C, int OH, int OW, int k, int s, int p,
+                                                          PoolBnr bnr = {}) {
     const uint32_t cpr = C / 8;
     const uint32_t total = (uint32_t)N * H * W * cpr;
+    // BNR: the thread's channel chunk is fixed (256 % cpr == 0, host check)
+    const int cfix = (int)((blockIdx.x * 256u + threadIdx.x) % cpr) * 8;
+    float mean[8], rstd[8], sc[8], sh[8], sgx[8], sg[8];
+    if constexpr (BNR) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            mean[i] = bnr.save[cfix + i];
+            rstd[i] = bnr.save[C + cfix + i];
+            sc[i] = rstd[i] * bnr.gamma[cfix + i];
+            sh[i] = bnr.beta[cfix + i] - mean[i] * sc[i];
+            sgx[i] = sg[i] = 0.f;
+        }
+    }
     for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
         const uint32_t pix = t / cpr, ch = t - pix * cpr;
         const uint32_t row = pix / (uint32_t)W, iw = pix - row * W;
@@ -159,10 +186,46 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
                 }
             }
         }
+        if constexpr (BNR) {  // ReLU mask from x, statistics of the stored (bf16) gradient
+            const u32x4 xw = *reinterpret_cast<const u32x4*>(bnr.x + (size_t)pix * C + ch * 8);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float xv = i & 1 ? hi_bf(xw[i >> 1]) : lo_bf(xw[i >> 1]);
+                if (!(fmaf(xv, sc[i], sh[i]) > 0.f)) acc[i] = 0.f;
+                const float gq = bf2f(f2bf(acc[i]));
+                sg[i] += gq;
+                sgx[i] += gq * ((xv - mean[i]) * rstd[i]);
+            }
+        }
         u32x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = pack_bf2(acc[2 * i], acc[2 * i + 1]);
         *reinterpret_cast<u32x4*>(dx + (size_t)pix * C + ch * 8) = o;
+    }
+    if constexpr (BNR) {
+        // lanes sharing a channel chunk: xor-fold over lane offsets cpr .. 32,
+        // then LDS adds across the block's waves, one global atomic per
+        // channel and quantity into the block's slab slot
+        __shared__ float red[2][2048];
+        const int lane = threadIdx.x & 63;
+        for (int c = threadIdx.x; c < 2 * C; c += 256) red[c / C][c % C] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            for (int o2 = (int)cpr; o2 < 64; o2 <<= 1) {
+                sg[i] += __shfl_xor(sg[i], o2, 64);
+                sgx[i] += __shfl_xor(sgx[i], o2, 64);
+            }
+        __syncthreads();
+        if (lane < (int)cpr) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                atomicAdd(&red[0][cfix + i], sgx[i]);
+                atomicAdd(&red[1][cfix + i], sg[i]);
+            }
+        }
+        __syncthreads();
+        float* slot = bnr.slab + (size_t)(blockIdx.x & 31) * 3 * C;
+        for (int c = threadIdx.x; c < 2 * C; c += 256) atomicAdd(slot + (c / C) * C + c % C, red[c / C][c % C]);
     }
 }
 
@@ -427,6 +490,22 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
     else
         hipLaunchKernelGGL(maxpool_bwd_kernel<0>, g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
                            (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// maxpool backward fused with the BN(+ReLU) backward reductions of the BN that
+// feeds the pool (the stem): dx = ReLU-masked gradient, slab += (sum g*xhat, sum g)
+IMK_EXPORT int imk_maxpool_bwd_bnr(const void* dy, const void* idx, void* dx, const void* x, const float* save,
+                                   const float* gamma, const float* beta, float* slab, int N, int H, int W,
+                                   int C, int OH, int OW, int k, int s, int p, void* stream) {
+    if (C % 8 || C > 2048 || 256 % (C / 8) || (k + s - 1) / s > 2) return -100;
+    const long total = (long)N * H * W * (C / 8);
+    if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    const dim3 g(stream_grid(total)), b(256);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<2, true>), g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p,
+                       PoolBnr{(const bf16_t*)x, save, gamma, beta, slab});
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -13,6 +13,8 @@ forward (:class:`Fp8State`).
 
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 from typing import List, Optional, Sequence
 
@@ -22,7 +24,7 @@ from ..ops import _lib
 from ..ops.block import BlockFn
 from ..ops.bn import BNActFn, bn_eval, running_update
 from ..ops.conv import ConvFn, LinearFn, igemm_fwd
-from ..ops.misc import AvgPoolFn, MaxPoolFn, TransposePlan, maxpool_eval
+from ..ops.misc import AvgPoolFn, BNReluPoolFn, MaxPoolFn, TransposePlan, maxpool_eval
 from .arena import ParamArena
 from .resnet import BasicBlock, BatchNorm2d, BNWork, Bottleneck, Conv2d, Linear, ResNet
 
@@ -252,6 +254,11 @@ def _conv(x, conv: Conv2d, bn: Optional[BatchNorm2d], train: bool):
                      stem=getattr(conv, "stem", False))
 
 
+# IMAGENT_STEM_FUSE=0: the stem's BN+ReLU and maxpool as separate autograd
+# nodes (pool backward, BN reduce, BN apply) -- A/B switch
+_FUSED_STEM = os.environ.get("IMAGENT_STEM_FUSE", "1") != "0"
+
+
 def _bn(x, bn, relu, train, x2=None, bn2=None, mode=0):
     if train:
         return BNActFn.apply(x, x2, bn, bn2, mode, relu)
@@ -275,8 +282,11 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     rows = []
     y = _conv(x, model.conv1, model.bn1, train)
     rows.append(y.numel() // y.shape[-1])
-    y = _bn(y, model.bn1, True, train)
-    y = MaxPoolFn.apply(y, 3, 2, 1) if train else maxpool_eval(y, 3, 2, 1)
+    if _FUSED_STEM:  # BN+ReLU+maxpool, backward fused (ops.misc.BNReluPoolFn)
+        y = BNReluPoolFn.apply(y, model.bn1, 3, 2, 1)
+    else:
+        y = _bn(y, model.bn1, True, train)
+        y = MaxPoolFn.apply(y, 3, 2, 1)
     if q is not None:
         q8 = q.out_for(y, q.pool_slot)
         if q8 is not None:

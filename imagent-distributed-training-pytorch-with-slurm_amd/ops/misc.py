@@ -36,6 +36,46 @@ class MaxPoolFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+class BNReluPoolFn(torch.autograd.Function):
+    """y = maxpool(relu(bn(x))) for the stem, with the backward fused across
+    the two ops: the pool backward stores the ReLU-masked BN upstream gradient
+    and reduces the BN-backward sums in the same pass
+    (``imk_maxpool_bwd_bnr``), then one BN apply pass -- instead of pool
+    backward + BN reduce + BN apply. The BN output is not kept for backward.
+    Reference ops: torchvision resnet ``bn1 -> relu -> maxpool``
+    (/root/reference/imagenet.py:312)."""
+
+    @staticmethod
+    def forward(ctx, x, bn, k, s, p):
+        from .bn import bn_act_forward
+        h = bn_act_forward(x, None, bn, None, 0, True)
+        N, H, W, Cc = h.shape
+        OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
+        y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
+        idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
+        _lib.check(_lib.kernels().imk_maxpool_fwd(h.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W,
+                                                  Cc, OH, OW, k, s, p, _lib.stream_ptr()), "maxpool")
+        ctx.save_for_backward(x, idx)
+        ctx.bn = bn
+        ctx.geom = (N, H, W, Cc, OH, OW, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .bn import bn_apply_backward
+        x, idx = ctx.saved_tensors
+        bn = ctx.bn
+        N, H, W, Cc, OH, OW, k, s, p = ctx.geom
+        g = torch.empty((N, H, W, Cc), device=dy.device, dtype=torch.bfloat16)
+        w = bn.work
+        _lib.check(_lib.kernels().imk_maxpool_bwd_bnr(
+            dy.contiguous().data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(), w.save.data_ptr(),
+            bn.weight.data_ptr(), bn.bias.data_ptr(), w.scratch.data_ptr(), N, H, W, Cc, OH, OW, k, s, p,
+            _lib.stream_ptr()), "maxpool bwd + bn reduce")
+        dx, _ = bn_apply_backward(g, x, None, bn, None, 0)
+        return dx, None, None, None, None
+
+
 def maxpool_eval(x, k, s, p):
     N, H, W, Cc = x.shape
     OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)

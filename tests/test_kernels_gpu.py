@@ -490,3 +490,37 @@ def test_conv_fp8_dgrad(shape, accum):
                      fp8=(nhwc(g8.view(torch.uint8)), e[0:1], wt8, e[1:2]))
     ref = nhwc(xr.grad) + (base.float() if accum else 0)
     assert rel(dx, ref) < 1e-2
+
+
+def test_maxpool_bwd_bn_reduce_fused():
+    """imk_maxpool_bwd_bnr: pool backward + ReLU mask from x + BN-backward sums."""
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.misc import MaxPoolFn
+    torch.manual_seed(7)
+    N, H, C = 4, 30, 64
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    mean, rstd = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.2
+    h = torch.relu((x.float() - mean) * rstd * gamma + beta).to(torch.bfloat16).requires_grad_(True)
+    y = MaxPoolFn.apply(h, 3, 2, 1)
+    dy = bf(torch.randn_like(y.float()))
+    y.backward(dy)
+    g_ref = h.grad.float() * ((x.float() - mean) * rstd * gamma + beta > 0)
+    OH = y.shape[1]
+    idx = torch.empty(y.shape, dtype=torch.uint8, device=DEV)
+    tmp = torch.empty_like(y)
+    _lib.check(_lib.kernels().imk_maxpool_fwd(h.detach().data_ptr(), tmp.data_ptr(), idx.data_ptr(), N, H, H, C,
+                                              OH, OH, 3, 2, 1, _lib.stream_ptr()), "pool")
+    save = torch.stack([mean, rstd]).contiguous()
+    slab = torch.zeros(32, 3, C, device=DEV)
+    g = torch.empty_like(x)
+    _lib.check(_lib.kernels().imk_maxpool_bwd_bnr(dy.data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(),
+                                                  save.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                                  slab.data_ptr(), N, H, H, C, OH, OH, 3, 2, 1,
+                                                  _lib.stream_ptr()), "pool bwd bnr")
+    assert rel(g, g_ref) < 1e-2
+    gb = g.float()
+    xhat = (x.float() - mean) * rstd
+    s = slab.sum(0)
+    assert rel(s[0], (gb * xhat).sum((0, 1, 2))) < 1e-3
+    assert rel(s[1], gb.sum((0, 1, 2))) < 1e-3

@@ -244,3 +244,50 @@ def test_graphed_step_matches_eager():
     assert step.replays == 2
     upd_graph = st.arena.P - state[0]
     assert rel(upd_graph, upd_eager) < 2e-2
+
+
+
+def test_fused_stem_pool_backward_matches_unfused():
+    """Stem BN+ReLU+maxpool as one node (pool backward with the BN reductions
+    fused, BNReluPoolFn) vs separate BN and pool nodes, same upstream gradient:
+    same input gradient and BN parameter gradients. (A whole random-init
+    network is too ill-conditioned at test batch sizes to compare two runs:
+    atomic-order noise alone moves its gradients.)"""
+    from imagent_amd.models.resnet import BatchNorm2d, BNWork
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.bn import BNActFn
+    from imagent_amd.ops.misc import BNReluPoolFn, MaxPoolFn
+    torch.manual_seed(5)
+    N, H, C = 8, 40, 64
+    x0 = (torch.randn(N, H, H, C, device=DEV) * 2 + 0.3).to(torch.bfloat16)
+    bn = BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    nbw = _lib.kernels().imk_bn_bwd_scratch_floats(1)
+    slab = torch.zeros(_lib.STAT_SLOTS, 2, C, device=DEV)
+    xf = x0.float().reshape(-1, C)
+    dy = None
+    out = []
+    for fused in (False, True):
+        slab.zero_()
+        slab[0, 0] = xf.sum(0)
+        slab[0, 1] = (xf * xf).sum(0)
+        bn.work = BNWork(slab, torch.zeros(2, C, device=DEV), torch.zeros(2, C, device=DEV),
+                         torch.zeros(nbw * C, device=DEV))
+        bn.weight.grad = torch.zeros_like(bn.weight)
+        bn.bias.grad = torch.zeros_like(bn.bias)
+        x = x0.clone().requires_grad_(True)
+        if fused:
+            y = BNReluPoolFn.apply(x, bn, 3, 2, 1)
+        else:
+            y = MaxPoolFn.apply(BNActFn.apply(x, None, bn, None, 0, True), 3, 2, 1)
+        if dy is None:
+            dy = torch.randn_like(y.float()).to(torch.bfloat16)
+        y.backward(dy)
+        out.append((y.detach().float(), x.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    (y0, g0, w0, b0), (y1, g1, w1, b1) = out
+    assert torch.equal(y0, y1)
+    assert rel(g1, g0) < 5e-3
+    assert rel(w1, w0) < 1e-3
+    assert rel(b1, b0) < 1e-3
