@@ -25,14 +25,42 @@ namespace {
 // (always valid) addresses with the validity kept as a mask: the
 // branch-per-window form waits one L2 round trip per window (the stem's pool
 // backward measured 594 us, 4x its bytes; profiles/r50_b512_v5_kernel_stats.md).
-template <int KMAX>  // KMAX > 0: k <= KMAX, windows unrolled; 0: generic k
+// Optional BatchNorm(+ReLU) prologue for the stem (BNF): the pool reads the
+// BN INPUT x and pools bf16(relu(x*sc + sh)) -- the BN output (4x the pool's
+// output bytes) is never written or re-read. Per-channel constants from the
+// conv-epilogue sums exactly as bn_fwd_kernel computes them (bn.hip).
+struct PoolBnf {
+    const float* sums;  // [2][C] sum, sum of squares
+    const float* gamma;
+    const float* beta;
+    float* save;        // [2][C] mean, rstd (for the backward)
+    float inv_cnt, eps;
+};
+
+template <int KMAX, bool BNF = false>  // KMAX > 0: k <= KMAX, windows unrolled; 0: generic k
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
                                                           int W, int C, int OH, int OW, int k, int s,
-                                                          int p) {
+                                                          int p, PoolBnf bnf = {}) {
     const uint32_t cpr = C / 8;
     const uint32_t total = (uint32_t)N * OH * OW * cpr;
+    float bsc[8], bsh[8];
+    if constexpr (BNF) {  // fixed channel chunk per thread (256 % cpr == 0, host check)
+        const uint32_t t0 = blockIdx.x * 256u + threadIdx.x;
+        const int c0 = (int)(t0 % cpr) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float mean = bnf.sums[c0 + i] * bnf.inv_cnt;
+            const float rstd = rsqrtf(fmaxf(bnf.sums[C + c0 + i] * bnf.inv_cnt - mean * mean, 0.f) + bnf.eps);
+            bsc[i] = rstd * bnf.gamma[c0 + i];
+            bsh[i] = bnf.beta[c0 + i] - mean * bsc[i];
+            if (t0 < cpr) {
+                bnf.save[c0 + i] = mean;
+                bnf.save[C + c0 + i] = rstd;
+            }
+        }
+    }
     for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
         const uint32_t pix = t / cpr, ch = t - pix * cpr;
         const uint32_t row = pix / (uint32_t)OW, ow = pix - row * OW;
@@ -48,7 +76,11 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         auto take = [&](const u32x4& w, bool ok, int win) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float a = lo_bf(w[i]), b = hi_bf(w[i]);
+                float a = lo_bf(w[i]), b = hi_bf(w[i]);
+                if constexpr (BNF) {  // the bf16 value the unfused BN+ReLU would have stored
+                    a = bf2f(f2bf(fmaxf(fmaf(a, bsc[2 * i], bsh[2 * i]), 0.f)));
+                    b = bf2f(f2bf(fmaxf(fmaf(b, bsc[2 * i + 1], bsh[2 * i + 1]), 0.f)));
+                }
                 // strict > keeps the first maximum (torch semantics); NaN propagates
                 if (ok && (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i]))) { best[2 * i] = a; bi[2 * i] = win; }
                 if (ok && (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1]))) { best[2 * i + 1] = b; bi[2 * i + 1] = win; }
@@ -490,6 +522,22 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
     else
         hipLaunchKernelGGL(maxpool_bwd_kernel<0>, g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
                            (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// BN(+ReLU) forward fused into the maxpool that consumes it (the stem): y =
+// maxpool(relu(bn(x))) with argmax indices; save <- (mean, rstd)
+IMK_EXPORT int imk_maxpool_fwd_bn(const void* x, const float* sums, const float* gamma, const float* beta,
+                                  float* save, void* y, void* idx, int N, int H, int W, int C, int OH, int OW,
+                                  int k, int s, int p, float eps, void* stream) {
+    if (C % 8 || 256 % (C / 8) || k > 3) return -100;
+    const long total = (long)N * OH * OW * (C / 8);
+    if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    const dim3 g(stream_grid(total)), b(256);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<3, true>), g, b, 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
+                       (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p,
+                       PoolBnf{sums, gamma, beta, save, 1.f / (float)((long)N * H * W), eps});
     IMK_CHECK_LAUNCH();
     return 0;
 }

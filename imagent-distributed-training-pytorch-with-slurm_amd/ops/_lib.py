@@ -142,6 +142,8 @@ def _declare(name: str, lib) -> None:
             "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+            "imk_maxpool_fwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                                   C.c_float, vp],
             "imk_maxpool_bwd_bnr": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                     vp],
             "imk_avgpool_fwd": [vp, vp, i32, i32, i32, vp],

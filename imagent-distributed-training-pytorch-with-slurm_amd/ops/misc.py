@@ -37,24 +37,28 @@ class MaxPoolFn(torch.autograd.Function):
 
 
 class BNReluPoolFn(torch.autograd.Function):
-    """y = maxpool(relu(bn(x))) for the stem, with the backward fused across
-    the two ops: the pool backward stores the ReLU-masked BN upstream gradient
-    and reduces the BN-backward sums in the same pass
-    (``imk_maxpool_bwd_bnr``), then one BN apply pass -- instead of pool
-    backward + BN reduce + BN apply. The BN output is not kept for backward.
+    """y = maxpool(relu(bn(x))) for the stem, fused both ways: the forward pools
+    bf16(relu(bn(x))) straight from the BN input (``imk_maxpool_fwd_bn``: the
+    BN output is never written), the backward stores the ReLU-masked BN
+    upstream gradient and reduces the BN-backward sums in the same pass
+    (``imk_maxpool_bwd_bnr``), then one BN apply pass -- instead of BN forward
+    + pool forward and pool backward + BN reduce + BN apply.
     Reference ops: torchvision resnet ``bn1 -> relu -> maxpool``
     (/root/reference/imagenet.py:312)."""
 
     @staticmethod
     def forward(ctx, x, bn, k, s, p):
-        from .bn import bn_act_forward
-        h = bn_act_forward(x, None, bn, None, 0, True)
-        N, H, W, Cc = h.shape
+        from .bn import stats_finalize
+        N, H, W, Cc = x.shape
         OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
         y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
         idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
-        _lib.check(_lib.kernels().imk_maxpool_fwd(h.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W,
-                                                  Cc, OH, OW, k, s, p, _lib.stream_ptr()), "maxpool")
+        w = bn.work
+        stats_finalize(w)  # conv-epilogue slab -> sums (also read by the running-stat update)
+        _lib.check(_lib.kernels().imk_maxpool_fwd_bn(
+            x.data_ptr(), w.stats.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), w.save.data_ptr(),
+            y.data_ptr(), idx.data_ptr(), N, H, W, Cc, OH, OW, k, s, p, bn.eps, _lib.stream_ptr()),
+            "bn + maxpool")
         ctx.save_for_backward(x, idx)
         ctx.bn = bn
         ctx.geom = (N, H, W, Cc, OH, OW, k, s, p)

@@ -243,7 +243,18 @@ def test_graphed_step_matches_eager():
     torch.cuda.synchronize()
     assert step.replays == 2
     upd_graph = st.arena.P - state[0]
-    assert rel(upd_graph, upd_eager) < 2e-2
+    # Two EAGER steps from this state already differ: BN statistics are fp32
+    # atomic sums (order-nondeterministic, ~1e-7), which now and then move a
+    # bf16-rounded activation by one ulp, and BatchNorm affine gradients
+    # (sum g*xhat over a random-init network: a small difference of large
+    # sums) amplify that into 1e-3..1e-1 of their update (scripts/dev/
+    # race_hunt.py: bimodal, batch-size dependent, present with every kernel
+    # variant and with the weight-gradient stream off). A broken capture
+    # (stale inputs, dropped kernels) moves the update by O(1).
+    e = rel(upd_graph, upd_eager)
+    print("graph-vs-eager rel", e)
+    assert e < 0.15, e
+    assert upd_graph.abs().max() > 0
 
 
 
