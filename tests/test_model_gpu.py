@@ -251,9 +251,20 @@ def test_graphed_step_matches_eager():
     # race_hunt.py: bimodal, batch-size dependent, present with every kernel
     # variant and with the weight-gradient stream off). A broken capture
     # (stale inputs, dropped kernels) moves the update by O(1).
+    # (and the random-init network at batch 8 amplifies such flips towards
+    # the stem, test_multirank_gpu). The replayed update must point the same
+    # way at the same size: projection ratio ~1 over the weights and over the
+    # vectors; stale inputs or dropped kernels give ~0 or wildly off ratios.
+    worst = 0.0
+    for kind in (lambda p: p.dim() > 1, lambda p: p.dim() == 1):  # weights, then BN affine / biases
+        idx = [i for i, p in enumerate(model.parameters()) if kind(p)]
+        a_ = torch.cat([st.arena.flat_slice(upd_graph, i) for i in idx])
+        b_ = torch.cat([st.arena.flat_slice(upd_eager, i) for i in idx])
+        worst = max(worst, abs((a_ * b_).sum().item() / (b_ * b_).sum().item() - 1.0))
     e = rel(upd_graph, upd_eager)
-    print("graph-vs-eager rel", e)
-    assert e < 0.15, e
+    print("graph-vs-eager: worst |projection ratio - 1|", worst, "rel", e)
+    assert worst < 0.1, worst
+    assert e < 0.5, e
     assert upd_graph.abs().max() > 0
 
 
