@@ -358,7 +358,16 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
             return e ? atoi(e) : 128;
         }();
         if (pref == 0) return 1;
-        maxbn = pref >= 128 ? 128 : 64;
+        // measured in the R50 step (profiles/r50_b512_v6): the tiled kernels'
+        // staged BN-backward epilogue wins for K = 128 (535 vs 622 us) and
+        // with the second BN branch (1037 vs 1097 us); this kernel for K = 64
+        // with the y mask (893 vs 916 us). IMAGENT_STREAM_BNB=all: every case.
+        static const bool all = [] {
+            const char* e = getenv("IMAGENT_STREAM_BNB");
+            return e && e[0] == 'a';
+        }();
+        if (!all && (a.C != 64 || a.bnx2)) return 1;
+        maxbn = (pref >= 128 || all) ? 128 : 64;
     }
     if (bn == 0) bn = maxbn;
     while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
