@@ -524,3 +524,15 @@ def test_maxpool_bwd_bn_reduce_fused():
     s = slab.sum(0)
     assert rel(s[0], (gb * xhat).sum((0, 1, 2))) < 1e-3
     assert rel(s[1], gb.sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("R,Cc", [(512, 1000), (7, 10), (100, 64), (2048, 130)])
+def test_colsum_accumulates(R, Cc):
+    """fc bias gradient: out += column sums of a bf16 [R, C] matrix."""
+    from imagent_amd.ops.conv import colsum_into
+    torch.manual_seed(9)
+    x = bf(torch.randn(R, Cc, device=DEV))
+    out = torch.randn(Cc, device=DEV)
+    ref = out + x.float().sum(0)
+    colsum_into(x, out)
+    assert rel(out, ref) < 1e-5
