@@ -1,4 +1,4 @@
-// Streaming 1x1 convolution for SHORT reductions (K = C in {64, 128}), gfx950.
+// Streaming 1x1 convolution for SHORT reductions (K = C in {64, 128, 256}), gfx950.
 //
 // ResNet bottlenecks spend their 56x56 / 28x28 stages in 1x1 convolutions with
 // K = 64 or 128: the expansion conv3 (64 -> 256, 128 -> 512) forward, and the
@@ -380,5 +380,8 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         if (bn == 128) return launch_stream<128, 128, 2>(a, st);
         return launch_stream<128, 64, 2>(a, st);
     }
+    // K = 256 into <= 128 channels (bottleneck conv1 256 -> 64 / 128): 64-channel
+    // slices, plain epilogue
+    if (a.C == 256 && a.Nout <= 128 && !(a.flags & IG_BNBWD)) return launch_stream1<256, 64, 2, 0>(a, st);
     return 1;
 }

@@ -36,6 +36,8 @@ SHAPES = [
     (4, 128, 28, 512, 1),
     (3, 128, 11, 128, 1),
     (4, 64, 28, 128, 2),    # strided 1x1 (ResNet-18/34 downsample): pixel gather
+    (6, 256, 14, 64, 1),    # K = 256 into 64 channels
+    (3, 256, 13, 128, 1),   # K = 256, two 64-channel slices, ragged pixels
 ]
 
 
