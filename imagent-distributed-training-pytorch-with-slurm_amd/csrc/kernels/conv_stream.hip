@@ -366,7 +366,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
             const char* e = getenv("IMAGENT_STREAM_BNB");
             return e && e[0] == 'a';
         }();
-        if (!all && (a.C != 64 || a.bnx2)) return 1;
+        if (!all && ((a.C != 64 && a.C != 256) || a.bnx2)) return 1;
         maxbn = (pref >= 128 || all) ? 128 : 64;
     }
     if (bn == 0) bn = maxbn;
@@ -382,6 +382,9 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     }
     // K = 256 into <= 128 channels (bottleneck conv1 256 -> 64 / 128): 64-channel
     // slices, plain epilogue
-    if (a.C == 256 && a.Nout <= 128 && !(a.flags & IG_BNBWD)) return launch_stream1<256, 64, 2, 0>(a, st);
+    if (a.C == 256 && a.Nout <= 128) {
+        if (!(a.flags & IG_BNBWD)) return launch_stream1<256, 64, 2, 0>(a, st);
+        if (!a.bnx2) return a.bny ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
+    }
     return 1;
 }

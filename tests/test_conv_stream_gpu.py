@@ -72,7 +72,8 @@ def test_stream_fwd_accumulate():
 
 
 @pytest.mark.parametrize("variant", ["y_mask", "x_mask", "x2", "accum"])
-@pytest.mark.parametrize("shape", [(8, 64, 28, 256), (3, 128, 9, 512), (5, 64, 13, 64)])
+@pytest.mark.parametrize("shape", [(8, 64, 28, 256), (3, 128, 9, 512), (5, 64, 13, 64), (4, 256, 14, 64),
+                                   (3, 256, 9, 128)])
 def test_stream_dgrad_bnb_matches_tiled(shape, variant, stream_toggle):
     """dX = dY x W^T for a 1x1 conv with K = Cout in {64, 128}, through the
     IG_BNBWD epilogue: stored gradient and slab reductions must match the
