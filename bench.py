@@ -45,9 +45,11 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--arch", default="resnet50")
-    # 512/GPU: the MI355X's 288 GB hold it with room to spare and it fills the
-    # chip on the 7x7/14x14 stages (256: -12 %, 1024: +6 % img/s, profiles/README)
-    ap.add_argument("--batch-size", type=int, default=512, help="per GPU")
+    # 1024/GPU (global 8192 on a node, BASELINE.json's large-batch config): the
+    # per-GPU batch sized for 288 GB of HBM (~41 GiB peak). It fills the chip on
+    # the 7x7/14x14 stages and halves the all-reduce's share of each step
+    # (256: -15 %, 512: -4 % img/s on one GPU; README)
+    ap.add_argument("--batch-size", type=int, default=1024, help="per GPU")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=16.0)

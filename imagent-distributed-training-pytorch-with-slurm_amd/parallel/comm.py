@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 from typing import List, Optional
 
 import torch
@@ -127,15 +128,18 @@ class RcclCommunicator(Communicator):
         nbytes = self.L.imc_unique_id_bytes()
         if rank == 0:
             buf = C.create_string_buffer(nbytes)
-            self._chk(self.L.imc_get_unique_id(buf), "ncclGetUniqueId")
-            uid = buf.raw
+            rc = self.L.imc_get_unique_id(buf)
+            uid = buf.raw if rc == 0 else b""
             if store is not None and world_size > 1:
-                store.set(key, uid)
+                store.set(key, uid)  # an empty id tells the other ranks to fail with us, not wait
+            self._chk(rc, "ncclGetUniqueId")
         else:
             if store is None:
                 raise RuntimeError("RcclCommunicator needs a c10d store to bootstrap rank > 0")
             store.wait([key])
             uid = store.get(key)
+            if len(uid) != nbytes:
+                raise RuntimeError("rank 0 could not create an RCCL unique id")
         h = C.c_void_p()
         self._chk(self.L.imc_comm_init(uid, world_size, rank, self.device.index or 0, 64, C.byref(h)),
                   "ncclCommInitRank")
@@ -214,9 +218,17 @@ def make_communicator(ctx, kind: str = "auto") -> Communicator:
             kind = "torch"
         else:
             kind = "local"
+    kind = os.environ.get("IMAGENT_COMM", kind)  # operator override: rccl | torch | local
     if kind == "rccl":
         store = _default_store() if ctx.world_size > 1 else None
-        return RcclCommunicator(ctx.rank, ctx.world_size, ctx.device, store)
+        try:
+            return RcclCommunicator(ctx.rank, ctx.world_size, ctx.device, store)
+        except RuntimeError as e:
+            if ctx.world_size == 1 or not dist.is_initialized():
+                raise
+            # every rank fails the same ncclCommInitRank, so all of them fall back together
+            warnings.warn(f"own RCCL communicator unavailable ({e}); using the c10d process group")
+            return TorchCommunicator()
     if kind == "torch":
         return TorchCommunicator()
     return LocalCommunicator()
