@@ -49,7 +49,8 @@ def main(argv=None):
     # per-GPU batch sized for 288 GB of HBM (~41 GiB peak). It fills the chip on
     # the 7x7/14x14 stages and halves the all-reduce's share of each step
     # (256: -15 %, 512: -4 % img/s on one GPU; README)
-    ap.add_argument("--batch-size", type=int, default=1024, help="per GPU")
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per GPU (default 1024; 512 / 256 when the device has too little free HBM)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=16.0)
@@ -80,105 +81,130 @@ def main(argv=None):
     if topo.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the launcher reports world size {topo.world_size}")
     ctx = init_distributed(topo, "nccl", 600.0, verbose=False)
-    dev = ctx.device
-    torch.manual_seed(0)
-    model = resnet.build(a.arch)
-    order = list(reversed(range(len(list(model.parameters())))))
-    native = None
-    if a.kernels == "hip":
-        from imagent_amd.models.native import bind_native
-        native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8",
-                             wgrad_overlap=bool(a.wgrad_overlap))
-        arena = native.arena
-    else:
-        model.to(dev)
-        arena = ParamArena(list(model.named_parameters()), dev, order=order)
-    comm = make_communicator(ctx, "rccl" if a.kernels == "hip" else "torch" if ctx.world_size > 1 else "local")
-    ddp = DataParallel(model, arena, comm, bucket_cap_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
-                       rebuild_buckets=False)
-    if native is not None:  # compute shadows of the rank-0-broadcast masters
-        native.refresh_shadows(full=True)
-    after = native.refresh_shadows if native else None
-    if a.optimizer == "lars":
-        from imagent_amd.train.optim import FlatLARS
-        opt = FlatLARS(arena, lr=0.1 * a.batch_size * a.gpus / 256, momentum=0.9, weight_decay=5e-5, eta=1e-3,
-                       after_step=after)
-    else:
-        opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=after)
-    metrics = DeviceMetrics(dev)
-    runner = StepRunner(ddp, opt, metrics, a.kernels, 0.0,
-                        torch.bfloat16 if a.kernels == "torch" else None)
-    if a.kernels == "torch":
-        model.to(memory_format=torch.channels_last)
-    src = SyntheticImageNet(a.batch_size * 4, a.image_size, 1000, a.batch_size, dev, seed=0,
-                            rank=ctx.rank)
-    tf = InputTransform(a.kernels, (a.image_size, a.image_size), cpad=resnet.ResNet.STEM_CPAD)
-    model.train()
+    if os.environ.get("IMAGENT_MEM_FRACTION") and ctx.device.type == "cuda":  # cap this process's share of HBM
+        torch.cuda.set_per_process_memory_fraction(float(os.environ["IMAGENT_MEM_FRACTION"]), ctx.device)
+    if a.batch_size is None:
+        a.batch_size = 1024
+        if ctx.device.type == "cuda" and ctx.world_size == 1:
+            # a GPU shared with another job (seen on the dev pool: a neighbour holding up
+            # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.127 GiB
+            # per image with two steps in flight (130 GiB at 1024 for a 40.6 GiB peak,
+            # scripts/dev/g_inflight.sh), and below that it thrashes (hipMalloc retries every
+            # step). Multi-rank runs keep 1024 on every rank.
+            free = torch.cuda.mem_get_info(ctx.device)[0] / 2**30
+            frac = os.environ.get("IMAGENT_MEM_FRACTION")
+            if frac:
+                free = min(free, float(frac) * torch.cuda.get_device_properties(ctx.device).total_memory / 2**30)
+            while a.batch_size > 256 and 0.13 * a.batch_size > free:
+                a.batch_size //= 2
+            if a.batch_size != 1024:
+                print(f"bench: {free:.1f} GiB of HBM free, running {a.batch_size} img/GPU", file=sys.stderr,
+                      flush=True)
 
-    def one(u8, y):
-        runner.train_step([(tf(u8), y)])
+    def run():
+        dev = ctx.device
+        torch.manual_seed(0)
+        model = resnet.build(a.arch)
+        order = list(reversed(range(len(list(model.parameters())))))
+        native = None
+        if a.kernels == "hip":
+            from imagent_amd.models.native import bind_native
+            native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8",
+                                 wgrad_overlap=bool(a.wgrad_overlap))
+            arena = native.arena
+        else:
+            model.to(dev)
+            arena = ParamArena(list(model.named_parameters()), dev, order=order)
+        comm = make_communicator(ctx, "rccl" if a.kernels == "hip" else "torch" if ctx.world_size > 1 else "local")
+        ddp = DataParallel(model, arena, comm, bucket_cap_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
+                           rebuild_buckets=False)
+        if native is not None:  # compute shadows of the rank-0-broadcast masters
+            native.refresh_shadows(full=True)
+        after = native.refresh_shadows if native else None
+        if a.optimizer == "lars":
+            from imagent_amd.train.optim import FlatLARS
+            opt = FlatLARS(arena, lr=0.1 * a.batch_size * a.gpus / 256, momentum=0.9, weight_decay=5e-5, eta=1e-3,
+                           after_step=after)
+        else:
+            opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=after)
+        metrics = DeviceMetrics(dev)
+        runner = StepRunner(ddp, opt, metrics, a.kernels, 0.0,
+                            torch.bfloat16 if a.kernels == "torch" else None)
+        if a.kernels == "torch":
+            model.to(memory_format=torch.channels_last)
+        src = SyntheticImageNet(a.batch_size * 4, a.image_size, 1000, a.batch_size, dev, seed=0,
+                                rank=ctx.rank)
+        tf = InputTransform(a.kernels, (a.image_size, a.image_size), cpad=resnet.ResNet.STEM_CPAD)
+        model.train()
 
-    if a.graph:
+        def one(u8, y):
+            runner.train_step([(tf(u8), y)])
+
+        if a.graph:
+            if ctx.world_size > 1:
+                raise SystemExit("--graph is validated for one GPU only")
+            from imagent_amd.train.engine import GraphedStep
+            one = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr)
+
+        def steps(n):
+            for u8, y in src.batches(n):
+                one(u8, y)
+
+        steps(a.warmup)
+        ctx.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        steps(a.steps)
+        torch.cuda.synchronize(dev)
+        ctx.barrier()
+        t1 = time.perf_counter()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         if ctx.world_size > 1:
-            raise SystemExit("--graph is validated for one GPU only")
-        from imagent_amd.train.engine import GraphedStep
-        one = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr)
+            torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+        T = float(elapsed.item())
+        loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
+        value = a.gpus * a.batch_size * a.steps / T
+        base = BASELINES.get((a.arch, a.image_size))
+        if ctx.rank == 0:
+            out = {
+                "metric": f"images/sec (whole node) {_NAMES.get(a.arch, a.arch)} {a.image_size}x{a.image_size} DDP",
+                "value": round(value, 2),
+                "unit": "images/s",
+                "n_gpus": a.gpus,
+                "steps": a.steps,
+                "warmup": a.warmup,
+                "ms_per_step": round(1000.0 * T / a.steps, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": round(value / base, 3) if base else None,
+                "dtype": "bf16" if a.dtype == "bf16" else "fp8 (e4m3 forward convs, bf16 backward)",
+                "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
+                        "random-init weights)",
+                "config": {
+                    "model": a.arch,
+                    "global_batch": a.batch_size * a.gpus,
+                    "per_gpu_batch": a.batch_size,
+                    "image_size": a.image_size,
+                    "seq_len": None,
+                    "parallelism": f"dp{a.gpus}",
+                    "kernels": a.kernels,
+                    "hip_graph": bool(a.graph),
+                    "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
+                                 "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
+                    "grad_allreduce": "fp32 bucketed RCCL avg, side stream",
+                    "bucket_mb": a.bucket_mb,
+                    "mean_train_loss": round(loss, 4),
+                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
+                    "reserved_hbm_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1)
+                    if dev.type == "cuda" else None,
+                    "alloc_retries": int(torch.cuda.memory_stats(dev).get("num_alloc_retries", 0))
+                    if dev.type == "cuda" else None,
+                },
+            }
+            print(json.dumps(out), flush=True)
+        comm.close()
 
-    def steps(n):
-        for u8, y in src.batches(n):
-            one(u8, y)
-
-    steps(a.warmup)
-    ctx.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    steps(a.steps)
-    torch.cuda.synchronize(dev)
-    ctx.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if ctx.world_size > 1:
-        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
-    T = float(elapsed.item())
-    loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
-    value = a.gpus * a.batch_size * a.steps / T
-    base = BASELINES.get((a.arch, a.image_size))
-    if ctx.rank == 0:
-        out = {
-            "metric": f"images/sec (whole node) {_NAMES.get(a.arch, a.arch)} {a.image_size}x{a.image_size} DDP",
-            "value": round(value, 2),
-            "unit": "images/s",
-            "n_gpus": a.gpus,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1000.0 * T / a.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / base, 3) if base else None,
-            "dtype": "bf16" if a.dtype == "bf16" else "fp8 (e4m3 forward convs, bf16 backward)",
-            "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
-                    "random-init weights)",
-            "config": {
-                "model": a.arch,
-                "global_batch": a.batch_size * a.gpus,
-                "per_gpu_batch": a.batch_size,
-                "image_size": a.image_size,
-                "seq_len": None,
-                "parallelism": f"dp{a.gpus}",
-                "kernels": a.kernels,
-                "hip_graph": bool(a.graph),
-                "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
-                             "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
-                "grad_allreduce": "fp32 bucketed RCCL avg, side stream",
-                "bucket_mb": a.bucket_mb,
-                "mean_train_loss": round(loss, 4),
-                "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
-                "alloc_retries": int(torch.cuda.memory_stats(dev).get("num_alloc_retries", 0))
-                if dev.type == "cuda" else None,
-            },
-        }
-        print(json.dumps(out), flush=True)
-    comm.close()
+    run()
     ctx.shutdown()
 
 
