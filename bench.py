@@ -46,7 +46,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--arch", default="resnet50")
     # 1024/GPU (global 8192 on a node, BASELINE.json's large-batch config): the
-    # per-GPU batch sized for 288 GB of HBM (~41 GiB peak). It fills the chip on
+    # per-GPU batch sized for 288 GB of HBM (~46 GiB peak, ~53 GiB reserved). It fills the chip on
     # the 7x7/14x14 stages and halves the all-reduce's share of each step
     # (256: -15 %, 512: -4 % img/s on one GPU; README)
     ap.add_argument("--batch-size", type=int, default=None,
@@ -87,15 +87,15 @@ def main(argv=None):
         a.batch_size = 1024
         if ctx.device.type == "cuda" and ctx.world_size == 1:
             # a GPU shared with another job (seen on the dev pool: a neighbour holding up
-            # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.127 GiB
-            # per image with two steps in flight (130 GiB at 1024 for a 40.6 GiB peak,
-            # scripts/dev/g_inflight.sh), and below that it thrashes (hipMalloc retries every
-            # step). Multi-rank runs keep 1024 on every rank.
+            # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.052 GiB
+            # per image (52.7 GiB at 1024, scripts/dev/g_protect.sh) + 15 % headroom, and
+            # below that it thrashes (hipMalloc retries every step). Multi-rank runs keep
+            # 1024 on every rank.
             free = torch.cuda.mem_get_info(ctx.device)[0] / 2**30
             frac = os.environ.get("IMAGENT_MEM_FRACTION")
             if frac:
                 free = min(free, float(frac) * torch.cuda.get_device_properties(ctx.device).total_memory / 2**30)
-            while a.batch_size > 256 and 0.13 * a.batch_size > free:
+            while a.batch_size > 256 and 0.06 * a.batch_size > free:
                 a.batch_size //= 2
             if a.batch_size != 1024:
                 print(f"bench: {free:.1f} GiB of HBM free, running {a.batch_size} img/GPU", file=sys.stderr,
