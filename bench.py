@@ -5,7 +5,9 @@ BASELINE.json metric: "images/sec (whole node) ResNet-50 224x224 DDP at
 4,337 R50@224-equivalent img/s for its whole 16-GPU job.
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1: launched by torch.distributed.run, one rank per GPU)
+    (N > 1: one rank per GPU. Under torch.distributed.run the ranks read
+    RANK/WORLD_SIZE/MASTER_*; run bare, bench.py starts torch.distributed.run
+    itself as a child process and forwards its output and exit code.)
 
 Each timed step is a complete training step on the hand-written MI355X
 path: GPU normalisation of synthetic uint8 images -> HIP forward (MFMA
@@ -39,6 +41,34 @@ _NAMES = {"resnet18": "ResNet-18", "resnet34": "ResNet-34", "resnet50": "ResNet-
           "resnet152": "ResNet-152"}
 
 
+def _self_launch(argv) -> int:
+    """``python bench.py --gpus N`` outside a launcher: run ``torch.distributed.run
+    --nproc-per-node N bench.py ...`` as a CHILD (this process never touched the
+    GPU, and is not replaced) and return its exit code. Rank 0's JSON line
+    reaches stdout through the child's inherited stdout (imagenet.sh:26 starts
+    one task per GPU with srun; this is the single-node equivalent)."""
+    import socket
+    import subprocess
+    a = [x for x in (argv if argv is not None else sys.argv[1:])]
+    n = None
+    for i, x in enumerate(a):
+        if x == "--gpus":
+            n = int(a[i + 1])
+        elif x.startswith("--gpus="):
+            n = int(x.split("=", 1)[1])
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + a
+    print("bench: launching " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +94,8 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward")
     a = ap.parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and "SLURM_PROCID" not in os.environ:
+        raise SystemExit(_self_launch(argv))
 
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.data.synthetic import SyntheticImageNet
@@ -81,14 +113,21 @@ def main(argv=None):
     if topo.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the launcher reports world size {topo.world_size}")
     ctx = init_distributed(topo, "nccl", 600.0, verbose=False)
+    on_gpu = ctx.device.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(ctx.device)
+
     if os.environ.get("IMAGENT_MEM_FRACTION") and ctx.device.type == "cuda":  # cap this process's share of HBM
         torch.cuda.set_per_process_memory_fraction(float(os.environ["IMAGENT_MEM_FRACTION"]), ctx.device)
+    auto_reduced = False
     if a.batch_size is None:
         a.batch_size = 1024
         if ctx.device.type == "cuda" and ctx.world_size == 1:
             # a GPU shared with another job (seen on the dev pool: a neighbour holding up
             # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.052 GiB
-            # per image (52.7 GiB at 1024, scripts/dev/g_protect.sh) + 15 % headroom, and
+            # per image (52.7 GiB at 1024, profiles/r50_b1024_allocator.md) + 15 % headroom, and
             # below that it thrashes (hipMalloc retries every step). Multi-rank runs keep
             # 1024 on every rank.
             free = torch.cuda.mem_get_info(ctx.device)[0] / 2**30
@@ -98,6 +137,7 @@ def main(argv=None):
             while a.batch_size > 256 and 0.06 * a.batch_size > free:
                 a.batch_size //= 2
             if a.batch_size != 1024:
+                auto_reduced = True
                 print(f"bench: {free:.1f} GiB of HBM free, running {a.batch_size} img/GPU", file=sys.stderr,
                       flush=True)
 
@@ -152,12 +192,14 @@ def main(argv=None):
 
         steps(a.warmup)
         ctx.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
+        c0 = comm.collectives
         t0 = time.perf_counter()
         steps(a.steps)
-        torch.cuda.synchronize(dev)
+        sync()
         ctx.barrier()
         t1 = time.perf_counter()
+        coll_per_step = (comm.collectives - c0) / max(1, a.steps)
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
         if ctx.world_size > 1:
             torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
@@ -177,7 +219,8 @@ def main(argv=None):
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": round(value / base, 3) if base else None,
-                "dtype": "bf16" if a.dtype == "bf16" else "fp8 (e4m3 forward convs, bf16 backward)",
+                "dtype": ("fp32" if not on_gpu else "bf16" if a.dtype == "bf16" else
+                          "fp8 (e4m3 forward convs, bf16 backward)"),
                 "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
                         "random-init weights)",
                 "config": {
@@ -191,7 +234,15 @@ def main(argv=None):
                     "hip_graph": bool(a.graph),
                     "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
                                  "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
-                    "grad_allreduce": "fp32 bucketed RCCL avg, side stream",
+                    "grad_allreduce": (f"fp32 bucketed {comm.name} avg on the comm stream, "
+                                       f"{coll_per_step:g} collectives/step" if coll_per_step > 0 else
+                                       "none (world of one, collectives skipped)"),
+                    "comm": comm.name,
+                    "world_size": ctx.world_size,
+                    "comm_nranks": getattr(comm, "nranks", comm.world_size),
+                    "collectives_per_step": coll_per_step,
+                    "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip",
+                    "auto_batch_reduced": auto_reduced,
                     "bucket_mb": a.bucket_mb,
                     "mean_train_loss": round(loss, 4),
                     "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,

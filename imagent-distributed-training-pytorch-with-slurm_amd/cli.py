@@ -44,6 +44,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--num-classes", type=int, default=1000, help="synthetic data only")
     p.add_argument("--synthetic-train-size", type=int, default=1281167)
     p.add_argument("--synthetic-val-size", type=int, default=50000)
+    p.add_argument("--synthetic-task", default="random", choices=["random", "colour"],
+                   help="random: uniform noise + labels (throughput); colour: learnable class-coloured images")
     p.add_argument("--flip", action="store_true", help="random horizontal flip (reference: none)")
     # --- optimisation ---
     p.add_argument("--optimizer", default="sgd",
@@ -74,7 +76,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hip-graph", action="store_true",
                    help="capture each training step in a HIP graph and replay it (1 GPU, step LR schedule)")
     p.add_argument("--step-timeout", type=float, default=0.0,
-                   help="dump all stacks if one training step exceeds this many seconds (hang detector)")
+                   help="hang watchdog: if no training / validation step completes for this many seconds, "
+                        "dump all stacks, abort the communicators and exit with status 75")
     p.add_argument("--check-consistency", type=int, default=0,
                    help="every N steps verify parameters are bit-identical across ranks")
     # --- logging / checkpoint ---

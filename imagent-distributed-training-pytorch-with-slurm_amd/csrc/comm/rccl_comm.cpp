@@ -7,8 +7,10 @@
 // MI355X-first choices:
 //  * one communicator per process (one process per GPU), bootstrapped from an
 //    ncclUniqueId that the Python side ships through the c10d TCPStore;
-//  * every collective runs on OUR comm stream, created at the highest stream
-//    priority, ordered after the producing compute stream by a HIP event and
+//  * every collective runs on OUR comm stream (normal priority: a high-priority
+//    queue parked on barrier packets throttles the compute queues, measured
+//    -15 % img/s, parallel/comm.py stream_mode), ordered after the producing
+//    compute stream by a HIP event and
 //    re-joined by one event wait before the optimizer step - no host syncs;
 //  * gradient buckets use ncclAvg (pre-scaling folded into the collective);
 //  * RCCL picks multi-channel rings / direct algorithms over the 7 xGMI links
@@ -51,7 +53,7 @@ thread_local char g_err[512] = {0};
 struct Comm {
     ncclComm_t comm = nullptr;
     hipStream_t stream = nullptr;
-    int rank = 0, nranks = 1, device = 0;
+    int rank = 0, nranks = 1, device = 0, n_events = 64, stream_mode = 0;
     std::vector<hipEvent_t> events;   // ring of reusable events
     size_t next_event = 0;
     hipEvent_t next() {
@@ -105,40 +107,157 @@ int32_t imc_version() {
     return v;
 }
 
-// Create the communicator and its comm stream on `device`.
-int32_t imc_comm_init(const char* id_bytes, int32_t nranks, int32_t rank, int32_t device,
-                      int32_t n_events, void** out) {
+// Wait out ncclInProgress on a non-blocking communicator (enqueue calls return
+// it while lazy connection set-up finishes in RCCL's own thread).
+static ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
+    while (r == ncclInProgress) {
+        ncclResult_t st = ncclSuccess;
+        ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+        if (q != ncclSuccess) return q;
+        r = st;
+    }
+    return r;
+}
+
+#define NCCLCALL(c, x)                                                                \
+    do {                                                                              \
+        ncclResult_t r_ = settle((c)->comm, (x));                                     \
+        if (r_ != ncclSuccess) {                                                      \
+            snprintf(g_err, sizeof(g_err), "%s: %s", #x, ncclGetErrorString(r_));     \
+            return -2;                                                                \
+        }                                                                             \
+    } while (0)
+
+// Start creating the communicator and its comm stream on `device`.
+// nonblocking != 0: ncclCommInitRankConfig(blocking = 0) returns at once and
+// imc_comm_poll() reports progress, so a rank whose peer failed can abort the
+// half-built communicator (imc_abort) instead of waiting in the bootstrap
+// forever. nonblocking == 0: classic blocking ncclCommInitRank.
+int32_t imc_comm_init_start(const char* id_bytes, int32_t nranks, int32_t rank, int32_t device,
+                            int32_t n_events, int32_t nonblocking, void** out) {
     HIPCHK(hipSetDevice(device));
     Comm* c = new Comm();
     c->rank = rank;
     c->nranks = nranks;
     c->device = device;
+    c->n_events = n_events < 4 ? 4 : n_events;
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
-    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
-    if (r != ncclSuccess) {
-        snprintf(g_err, sizeof(g_err), "ncclCommInitRank: %s", ncclGetErrorString(r));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = nonblocking ? 0 : 1;
+    ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        snprintf(g_err, sizeof(g_err), "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+        if (c->comm) ncclCommAbort(c->comm);
         delete c;
         return -2;
     }
-    int lo = 0, hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    // `hi` is the numerically smallest == highest priority.
-    HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
-    if (n_events < 4) n_events = 4;
-    c->events.resize(n_events);
-    for (auto& e : c->events) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return 0;
+}
+
+// Once the communicator is ready: create the comm stream and its events.
+// Created AFTER RCCL's own init (which makes its internal streams): HIP hands
+// streams to the GPU_MAX_HW_QUEUES hardware queues round-robin in creation
+// order, and creating ours first was measured to land the wgrad side stream
+// on a shared queue (R50/1024: 12.0k -> 10.6k img/s on one MI355X).
+// Stream kinds: 0 plain, 1 highest priority, 2 full-CU-mask stream (the HIP
+// runtime gives a CU-masked stream a hardware queue of its own instead of
+// sharing one of the GPU_MAX_HW_QUEUES round-robin queues, so a barrier packet
+// on it can never stall another stream's kernels queued behind it).
+static int32_t create_stream(int32_t mode, hipStream_t* out) {
+    if (mode == 2) {
+        int dev = 0, ncu = 0;
+        HIPCHK(hipGetDevice(&dev));
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0xffffffffu);
+        HIPCHK(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
+        return 0;
+    }
+    if (mode == 1) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        // `hi` is the numerically smallest == highest priority.
+        HIPCHK(hipStreamCreateWithPriority(out, hipStreamNonBlocking, hi));
+        return 0;
+    }
+    HIPCHK(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    return 0;
+}
+
+static int32_t finish_setup(Comm* c) {
+    if (c->stream) return 0;
+    int32_t rc = create_stream(c->stream_mode, &c->stream);
+    if (rc) return rc;
+    c->events.resize(c->n_events);
+    for (auto& e : c->events) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return 0;
+}
+
+// Kind of comm stream finish_setup() creates (see create_stream); call before
+// the communicator is ready.
+int32_t imc_comm_set_stream_mode(void* h, int32_t mode) {
+    static_cast<Comm*>(h)->stream_mode = mode;
+    return 0;
+}
+
+// A stream of the given kind for other users (the weight-gradient side stream).
+int32_t imc_stream_create(int32_t device, int32_t mode, void** out) {
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    int32_t rc = create_stream(mode, &s);
+    *out = s;
+    return rc;
+}
+
+int32_t imc_stream_destroy(void* s) {
+    HIPCHK(hipStreamDestroy((hipStream_t)s));
+    return 0;
+}
+
+// 0: ready, 1: still initialising, < 0: failed (message in imc_last_error).
+int32_t imc_comm_poll(void* h) {
+    Comm* c = static_cast<Comm*>(h);
+    if (!c || !c->comm) {
+        snprintf(g_err, sizeof(g_err), "communicator aborted");
+        return -3;
+    }
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t q = ncclCommGetAsyncError(c->comm, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclInProgress) return 1;
+    if (st != ncclSuccess) {
+        snprintf(g_err, sizeof(g_err), "ncclCommInitRank: %s", ncclGetErrorString(st));
+        return -2;
+    }
+    return finish_setup(c);
+}
+
+// Blocking creation (kept for tools): start + wait.
+int32_t imc_comm_init(const char* id_bytes, int32_t nranks, int32_t rank, int32_t device,
+                      int32_t n_events, void** out) {
+    int32_t rc = imc_comm_init_start(id_bytes, nranks, rank, device, n_events, 0, out);
+    return rc ? rc : imc_comm_poll(*out);
+}
+
+int32_t imc_comm_nranks(void* h) {
+    Comm* c = static_cast<Comm*>(h);
+    int n = -1;
+    if (c && c->comm && ncclCommCount(c->comm, &n) != ncclSuccess) n = -1;
+    return n;
 }
 
 int32_t imc_comm_destroy(void* h) {
     Comm* c = static_cast<Comm*>(h);
     if (!c) return 0;
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) {
+        // a non-blocking communicator finalises asynchronously
+        if (settle(c->comm, ncclCommFinalize(c->comm)) == ncclSuccess) ncclCommDestroy(c->comm);
+        else ncclCommAbort(c->comm);
+    }
     for (auto& e : c->events) (void)hipEventDestroy(e);
-    if (c->comm) ncclCommDestroy(c->comm);
-    (void)hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
 }
@@ -171,7 +290,7 @@ int32_t imc_allreduce(void* h, void* ptr, uint64_t count, int32_t dtype, int32_t
         int32_t rc = imc_stream_join_from(h, src);
         if (rc) return rc;
     }
-    NCCLCHK(ncclAllReduce(ptr, ptr, count, to_nccl(dtype), to_op(op), c->comm, c->stream));
+    NCCLCALL(c, ncclAllReduce(ptr, ptr, count, to_nccl(dtype), to_op(op), c->comm, c->stream));
     return 0;
 }
 
@@ -187,7 +306,7 @@ int32_t imc_allreduce_group(void* h, int32_t n, void** ptrs, const uint64_t* cou
     for (int32_t i = 0; i < n; ++i)
         NCCLCHK(ncclAllReduce(ptrs[i], ptrs[i], counts[i], to_nccl(dtype), to_op(op), c->comm,
                               c->stream));
-    NCCLCHK(ncclGroupEnd());
+    NCCLCALL(c, ncclGroupEnd());
     return 0;
 }
 
@@ -197,7 +316,7 @@ int32_t imc_broadcast(void* h, void* ptr, uint64_t count, int32_t dtype, int32_t
         int32_t rc = imc_stream_join_from(h, src);
         if (rc) return rc;
     }
-    NCCLCHK(ncclBroadcast(ptr, ptr, count, to_nccl(dtype), root, c->comm, c->stream));
+    NCCLCALL(c, ncclBroadcast(ptr, ptr, count, to_nccl(dtype), root, c->comm, c->stream));
     return 0;
 }
 
@@ -208,7 +327,7 @@ int32_t imc_allgather(void* h, const void* send, void* recv, uint64_t count, int
         int32_t rc = imc_stream_join_from(h, src);
         if (rc) return rc;
     }
-    NCCLCHK(ncclAllGather(send, recv, count, to_nccl(dtype), c->comm, c->stream));
+    NCCLCALL(c, ncclAllGather(send, recv, count, to_nccl(dtype), c->comm, c->stream));
     return 0;
 }
 
@@ -219,8 +338,8 @@ int32_t imc_reduce_scatter(void* h, const void* send, void* recv, uint64_t recv_
         int32_t rc = imc_stream_join_from(h, src);
         if (rc) return rc;
     }
-    NCCLCHK(ncclReduceScatter(send, recv, recv_count, to_nccl(dtype), to_op(op), c->comm,
-                              c->stream));
+    NCCLCALL(c, ncclReduceScatter(send, recv, recv_count, to_nccl(dtype), to_op(op), c->comm,
+                                  c->stream));
     return 0;
 }
 
@@ -234,9 +353,10 @@ int32_t imc_synchronize(void* h) {
 // state of the communicator (0 == ok).
 int32_t imc_async_error(void* h) {
     Comm* c = static_cast<Comm*>(h);
+    if (!c || !c->comm) return -3;  // aborted
     ncclResult_t st = ncclSuccess;
     ncclCommGetAsyncError(c->comm, &st);
-    return (int32_t)st;
+    return st == ncclInProgress ? 0 : (int32_t)st;
 }
 
 int32_t imc_abort(void* h) {

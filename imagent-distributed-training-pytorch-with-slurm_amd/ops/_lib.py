@@ -193,6 +193,12 @@ def _declare(name: str, lib) -> None:
         lib.imc_synchronize.argtypes = [vp]
         lib.imc_async_error.argtypes = [vp]
         lib.imc_abort.argtypes = [vp]
+        lib.imc_comm_init_start.argtypes = [C.c_char_p, i32, i32, i32, i32, i32, C.POINTER(vp)]
+        lib.imc_comm_poll.argtypes = [vp]
+        lib.imc_comm_nranks.argtypes = [vp]
+        lib.imc_comm_set_stream_mode.argtypes = [vp, i32]
+        lib.imc_stream_create.argtypes = [i32, i32, C.POINTER(vp)]
+        lib.imc_stream_destroy.argtypes = [vp]
     elif name == "runtime":
         lib.imr_plan_buckets.argtypes = [i32, C.POINTER(C.c_int64), C.c_int64, C.c_int64,
                                          C.POINTER(C.c_int32)]

@@ -8,8 +8,10 @@ second HIP stream lets it fill the CUs the critical-path kernels leave idle
 
 Dependencies that make this safe:
 * the side stream waits for the main stream before each wgrad (its inputs);
-* tensors read on the side stream are ``record_stream``-ed so the caching
-  allocator does not recycle them early;
+* tensors read on the side stream are held (:func:`protect`) until the
+  end-of-backward join, then released in main-stream order, so the caching
+  allocator cannot recycle them while a side-stream kernel still reads them
+  (``IMAGENT_PROTECT=record`` uses ``record_stream`` instead);
 * the data-parallel reducer makes each bucket's all-reduce wait for the side
   stream as well as the main one (``parallel/ddp.py``), and the end of
   backward joins the side stream into the main one (the optimizer reads the
@@ -43,9 +45,26 @@ def side_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.St
     idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
     s = _streams.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        s = _new_stream(idx)
         _streams[idx] = s
     return s
+
+
+def _new_stream(idx: int):
+    """A torch pool stream, or (``IMAGENT_QUEUE_MODE=dedicated``) a full-CU-mask
+    HIP stream that the runtime puts on a hardware queue of its own
+    (``parallel/comm.py`` ``stream_mode``: measured slower), kept for the
+    process lifetime."""
+    from ..parallel.comm import stream_mode
+    if stream_mode() != 2:
+        return torch.cuda.Stream(device=idx)
+    import ctypes as C
+    from . import _lib
+    h = C.c_void_p()
+    rc = _lib.comm().imc_stream_create(idx, 2, C.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"side stream: {_lib.comm().imc_last_error().decode()}")
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
 
 
 def active_side_stream() -> Optional[torch.cuda.Stream]:
@@ -60,17 +79,17 @@ _keep: list = []
 # main-stream order (immediately reusable), rather than record_stream'ed (freed
 # only once the allocator sees the side stream pass them, so with the CPU ahead
 # of the GPU every step got fresh blocks). Measured at R50 / 1024 img
-# (scripts/dev/g_protect.sh): reserved HBM 129 -> 52.7 GiB, peak 40.6 -> 45.9 GiB,
+# (profiles/r50_b1024_allocator.md): reserved HBM 129 -> 52.7 GiB, peak 40.6 -> 45.9 GiB,
 # img/s unchanged. IMAGENT_PROTECT=record restores record_stream.
 _KEEP_EAGER = os.environ.get("IMAGENT_PROTECT", "keep") == "keep"
 
 
 def protect(*tensors: torch.Tensor) -> None:
-    """Keep tensors read on the side stream from being recycled too early:
-    ``record_stream`` in eager mode; while a HIP graph is being captured
-    (where ``record_stream`` is not usable) a reference is held until the
-    side stream has been joined back, which is also the dependency edge the
-    captured graph needs."""
+    """Keep tensors read on the side stream from being recycled too early: a
+    reference is held until the side stream has been joined back into the
+    main stream (default, and always while a HIP graph is being captured,
+    where ``record_stream`` is not usable; the join is also the dependency
+    edge a captured graph needs). ``IMAGENT_PROTECT=record``: ``record_stream``."""
     s = active_side_stream()
     if s is None:
         return
@@ -89,6 +108,21 @@ def join_side_into_current() -> None:
 
 
 _join_queued = False
+
+
+def held() -> int:
+    """Number of side-stream operands currently held (0 after every join)."""
+    return len(_keep)
+
+
+def reset() -> None:
+    """Start-of-step / failure-path reset: join anything still outstanding and
+    forget a join callback that a failed backward never ran (otherwise later
+    backwards would never queue their own join and ``_keep`` would grow)."""
+    global _join_queued
+    _join_queued = False
+    if _keep:
+        join_side_into_current()
 
 
 def _join_cb() -> None:

@@ -5,7 +5,7 @@ per-forward buffer broadcasts and three scalar metric all-reduces per step
 (``imagenet.py:84-86,137-139``).
 
 :class:`RcclCommunicator` owns its own RCCL communicator (bootstrapped through
-the c10d TCPStore) and a highest-priority HIP stream: collectives are ordered
+the c10d TCPStore) and its own HIP comm stream: collectives are ordered
 after the producing compute stream by an event and the compute stream joins
 back with one event wait before the optimizer step. :class:`TorchCommunicator`
 offers the same interface over ``torch.distributed`` (``gloo`` for CPU runs
@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 import warnings
 from typing import List, Optional
 
@@ -31,6 +32,7 @@ class Communicator:
     rank: int = 0
     world_size: int = 1
     name = "base"
+    collectives: int = 0  # collectives actually issued (0 for a world of one that skips them)
 
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> None:
         raise NotImplementedError
@@ -50,6 +52,9 @@ class Communicator:
     def healthy(self) -> bool:
         return True
 
+    def abort(self) -> None:
+        """Failure path: unblock collectives waiting on dead peers."""
+
     def close(self) -> None:
         pass
 
@@ -57,6 +62,23 @@ class Communicator:
         """Collectives issued after this call also wait for ``stream``."""
         if torch.cuda.is_available():
             torch.cuda.current_stream().wait_stream(stream)
+
+
+def stream_mode() -> int:
+    """Kind of HIP stream for the comm stream (and the weight-gradient side
+    stream), ``IMAGENT_QUEUE_MODE``:
+
+    * ``plain`` (default): normal priority;
+    * ``priority``: highest-priority comm stream. Measured on one MI355X at
+      R50 / 1024 img with RCCL self collectives: 10.2k vs 12.1k img/s. The comm
+      stream spends the backward parked on barrier packets (waiting for the
+      next bucket's producers); while a high-priority queue holds work the
+      lower-priority queues' wave launches are throttled, and the main-stream
+      forward / BN kernels ran 10-40 % slower (stats_finalize 5x);
+    * ``dedicated``: full-CU-mask streams (a hardware queue each): 8.9k img/s.
+
+    Study: ``profiles/r50_b1024_comm_stream_study.md``."""
+    return {"dedicated": 2, "priority": 1, "plain": 0}[os.environ.get("IMAGENT_QUEUE_MODE", "plain")]
 
 
 class LocalCommunicator(Communicator):
@@ -87,6 +109,7 @@ class TorchCommunicator(Communicator):
     def allreduce_(self, t, op="sum"):
         if self.world_size == 1:
             return
+        self.collectives += 1
         if op == "avg" and self.backend != "nccl":
             w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self._pending.append((w, t))
@@ -112,38 +135,112 @@ class TorchCommunicator(Communicator):
                 div.div_(self.world_size)
         self._pending.clear()
 
+    def abort(self):
+        try:
+            dist.distributed_c10d._abort_process_group()
+        except Exception:  # best effort: the process exits right after
+            pass
+
 
 class RcclCommunicator(Communicator):
-    """Our own RCCL communicator on a dedicated high-priority HIP stream."""
+    """Our own RCCL communicator on its own HIP comm stream (normal priority:
+    see :func:`stream_mode`).
+
+    Bootstrap (multi-rank): rank 0 publishes the ncclUniqueId through the c10d
+    store; every rank starts a NON-BLOCKING ``ncclCommInitRankConfig`` and polls
+    it while watching the store for a failure flag. A rank whose init fails
+    (or times out) raises the flag before raising, so its peers abort their
+    half-built communicators instead of waiting in the RCCL bootstrap, and all
+    ranks fall back together (:func:`make_communicator`). A rank that finished
+    also waits until every rank reports success, so no rank starts issuing
+    RCCL collectives while another has fallen back to c10d.
+
+    ``self_collectives`` (default on, ``IMAGENT_RCCL_SELF=0`` turns it off):
+    at world size 1 the collectives are still issued to RCCL (a one-rank
+    communicator), so the single-GPU run exercises exactly the comm-stream
+    ordering, events and buffer lifetimes of the multi-GPU one.
+    """
 
     name = "rccl"
+    _instances = 0  # per-process creation counter: every rank creates communicators in the same order
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None,
-                 key: str = "imagent/rccl_uid"):
+                 key: Optional[str] = None, self_collectives: Optional[bool] = None,
+                 nonblocking: Optional[bool] = None, init_timeout: float = 600.0):
         from ..ops import _lib
         self._lib = _lib
         self.L = _lib.comm()
         self.rank, self.world_size = rank, world_size
         self.device = torch.device(device)
+        self.h = None
+        if self_collectives is None:
+            self_collectives = os.environ.get("IMAGENT_RCCL_SELF", "1") != "0"
+        if nonblocking is None:
+            nonblocking = os.environ.get("IMAGENT_RCCL_NONBLOCKING", "1") != "0"
+        self.active = world_size > 1 or bool(self_collectives)
+        self.collectives = 0  # collectives handed to RCCL so far
+        self._held: List[torch.Tensor] = []
+        RcclCommunicator._instances += 1
+        key = key or f"imagent/rccl/{RcclCommunicator._instances}"
+        multi = store is not None and world_size > 1
+        if world_size > 1 and store is None:
+            raise RuntimeError("RcclCommunicator needs a c10d store to bootstrap a multi-rank job")
+        fail_key = f"{key}/fail"
+
+        def fail(msg: str):
+            if multi:
+                store.set(fail_key, f"rank {rank}: {msg}")  # peers abort instead of waiting on us
+            raise RuntimeError(msg)
+
         nbytes = self.L.imc_unique_id_bytes()
         if rank == 0:
             buf = C.create_string_buffer(nbytes)
             rc = self.L.imc_get_unique_id(buf)
             uid = buf.raw if rc == 0 else b""
-            if store is not None and world_size > 1:
-                store.set(key, uid)  # an empty id tells the other ranks to fail with us, not wait
-            self._chk(rc, "ncclGetUniqueId")
+            if multi:
+                store.set(f"{key}/uid", uid)  # an empty id tells the other ranks to fail with us
+            if rc != 0:
+                fail(f"ncclGetUniqueId: {self.L.imc_last_error().decode()}")
         else:
-            if store is None:
-                raise RuntimeError("RcclCommunicator needs a c10d store to bootstrap rank > 0")
-            store.wait([key])
-            uid = store.get(key)
+            store.wait([f"{key}/uid"])
+            uid = store.get(f"{key}/uid")
             if len(uid) != nbytes:
                 raise RuntimeError("rank 0 could not create an RCCL unique id")
         h = C.c_void_p()
-        self._chk(self.L.imc_comm_init(uid, world_size, rank, self.device.index or 0, 64, C.byref(h)),
-                  "ncclCommInitRank")
+        rc = self.L.imc_comm_init_start(uid, world_size, rank, self.device.index or 0, 64, int(nonblocking),
+                                        C.byref(h))
+        if rc != 0:
+            fail(f"ncclCommInitRank: {self.L.imc_last_error().decode()} (rc={rc})")
         self.h = h
+        self.L.imc_comm_set_stream_mode(h, stream_mode())
+        t0 = time.monotonic()
+        delay = 1e-4
+        while True:  # non-blocking init: poll, and watch for a peer's failure
+            rc = self.L.imc_comm_poll(h)
+            if rc == 0:
+                break
+            if rc < 0:
+                msg = self.L.imc_last_error().decode()
+                self.abort()
+                fail(f"{msg} (rc={rc})")
+            if multi and store.check([fail_key]):
+                self.abort()
+                raise RuntimeError(f"RCCL init abandoned: {store.get(fail_key).decode()}")
+            if time.monotonic() - t0 > init_timeout:
+                self.abort()
+                fail(f"ncclCommInitRank did not finish within {init_timeout:.0f} s")
+            time.sleep(delay)
+            delay = min(delay * 2, 0.01)
+        if multi:  # agreement: nobody proceeds until every rank holds a working communicator
+            store.add(f"{key}/ok", 1)
+            while store.add(f"{key}/ok", 0) < world_size:
+                if store.check([fail_key]):
+                    self.abort()
+                    raise RuntimeError(f"RCCL init abandoned: {store.get(fail_key).decode()}")
+                if time.monotonic() - t0 > init_timeout:
+                    self.abort()
+                    fail(f"RCCL ranks did not all come up within {init_timeout:.0f} s")
+                time.sleep(0.001)
         self.stream = torch.cuda.ExternalStream(self.L.imc_comm_stream(h), device=self.device)
 
     def _chk(self, rc, what):
@@ -153,48 +250,71 @@ class RcclCommunicator(Communicator):
     def _cur(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    @property
+    def nranks(self) -> int:
+        """Ranks in the RCCL communicator as RCCL itself reports them."""
+        return int(self.L.imc_comm_nranks(self.h)) if self.h else 0
+
     def allreduce_(self, t, op="sum"):
         assert t.is_cuda and t.is_contiguous()
-        if self.world_size == 1:
-            return  # a one-rank all-reduce is the identity: skip the RCCL copy kernel
+        if not self.active:
+            return  # self collectives off: a one-rank all-reduce is the identity
         self._chk(self.L.imc_allreduce(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], self._cur()),
                   "allreduce")
-        # keep the tensor alive until the comm stream is done with it
-        t.record_stream(self.stream)
+        self.collectives += 1
+        self._held.append(t)  # alive until the caller's stream has joined the comm stream
 
     def broadcast_(self, t, root=0):
         assert t.is_cuda and t.is_contiguous()
+        if not self.active:
+            return
         self._chk(self.L.imc_broadcast(self.h, t.data_ptr(), t.numel(), _DT[t.dtype], root, self._cur()),
                   "broadcast")
-        t.record_stream(self.stream)
+        self.collectives += 1
+        self._held.append(t)
         self.join()
 
     def allgather(self, t):
         t = t.contiguous()
+        if not self.active:
+            return t.unsqueeze(0).clone()
         out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         self._chk(self.L.imc_allgather(self.h, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype],
                                        self._cur()), "allgather")
-        out.record_stream(self.stream)
+        self.collectives += 1
+        self._held.extend((t, out))
         self.join()
         return out
 
     def depend_on(self, stream) -> None:
-        if self.world_size > 1:  # the comm stream waits; the compute stream keeps going
+        if self.active:  # the comm stream waits; the compute stream keeps going
             self._chk(self.L.imc_stream_join_from(self.h, stream.cuda_stream), "join_from")
 
     def join(self):
-        self._chk(self.L.imc_stream_join_into(self.h, self._cur()), "join")
+        if self.h:
+            self._chk(self.L.imc_stream_join_into(self.h, self._cur()), "join")
+        # Operands are held rather than record_stream'ed on the comm stream: once the caller's
+        # stream waits for the comm stream, freeing them in the caller's stream order is safe,
+        # and no allocator block ever refers to the comm stream (which close() destroys).
+        self._held.clear()
 
     def synchronize(self):
         self._chk(self.L.imc_synchronize(self.h), "sync")
 
     def healthy(self) -> bool:
-        return self.L.imc_async_error(self.h) == 0
+        return bool(self.h) and self.L.imc_async_error(self.h) == 0
+
+    def abort(self) -> None:
+        """Tear the communicator down without waiting for peers (failure path):
+        any collective blocked on a dead rank returns with an error."""
+        if getattr(self, "h", None):
+            self.L.imc_abort(self.h)
 
     def close(self):
         if getattr(self, "h", None):
-            self.L.imc_comm_destroy(self.h)
+            self.L.imc_comm_destroy(self.h)  # synchronises the comm stream first
             self.h = None
+        self._held.clear()
 
 
 def _default_store():
@@ -226,7 +346,8 @@ def make_communicator(ctx, kind: str = "auto") -> Communicator:
         except RuntimeError as e:
             if ctx.world_size == 1 or not dist.is_initialized():
                 raise
-            # every rank fails the same ncclCommInitRank, so all of them fall back together
+            # the bootstrap's failure flag makes every rank fail together (RcclCommunicator),
+            # so all of them fall back to the c10d group together
             warnings.warn(f"own RCCL communicator unavailable ({e}); using the c10d process group")
             return TorchCommunicator()
     if kind == "torch":

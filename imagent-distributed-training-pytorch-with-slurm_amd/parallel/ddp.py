@@ -132,7 +132,8 @@ class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, arena: ParamArena, comm: Optional[Communicator] = None,
                  bucket_cap_mb: float = 16.0, first_bucket_mb: float = 2.0,
                  broadcast_buffers: str = "eval", rebuild_buckets: bool = True,
-                 find_unused_parameters: bool = False, use_autograd_hooks: Optional[bool] = None):
+                 find_unused_parameters: bool = False, use_autograd_hooks: Optional[bool] = None,
+                 probe_order: bool = False):
         super().__init__()
         self.module = module
         self.arena = arena
@@ -147,6 +148,10 @@ class DataParallel(nn.Module):
         self._callback_queued = False
         self._in_backward = False
         self.last_order: List[int] = []
+        # ordering probe (race detector): a checksum of every bucket taken ON
+        # the comm stream right after its all-reduce; see verify_order()
+        self.probe_order = probe_order
+        self._probe_sums: Optional[torch.Tensor] = None
 
         self._verify_and_broadcast()
         self._plan()
@@ -277,6 +282,45 @@ class DataParallel(nn.Module):
             # the all-reduce waits for it too (main stream not blocked)
             self.comm.depend_on(side)
         self.comm.allreduce_(self.arena.G[lo:hi], "avg")
+        if self.probe_order:
+            self._probe(b, lo, hi)
+
+    def _probe(self, b: int, lo: int, hi: int) -> None:
+        s = getattr(self.comm, "stream", None)
+        if s is None or not self.arena.G.is_cuda:
+            return
+        if self._probe_sums is None or self._probe_sums.numel() != len(self.buckets):
+            self._probe_sums = torch.full((len(self.buckets),), float("nan"), dtype=torch.float64,
+                                          device=self.arena.G.device)
+        with torch.cuda.stream(s):
+            torch.sum(self.arena.G[lo:hi].view(1, -1), dim=1, dtype=torch.float64,
+                      out=self._probe_sums.narrow(0, b, 1))
+
+    @torch.no_grad()
+    def verify_order(self) -> List[int]:
+        """Buckets whose all-reduce saw different data than the finished
+        gradient (call after the step, before the next ``zero_grad``).
+
+        The probe sums each bucket on the comm stream right after its
+        collective. If the collective was ordered after every kernel that
+        writes the bucket (main stream AND wgrad side stream), that checksum
+        equals the one of the final gradient bit for bit (same data, same
+        deterministic reduction); a bucket reduced before a producer finished
+        shows up as a mismatch. Returns the mismatching bucket ids."""
+        if self._probe_sums is None:
+            return []
+        torch.cuda.synchronize(self.arena.G.device)
+        got = self._probe_sums.clone()
+        want = torch.stack([self.arena.G[lo:hi].view(1, -1).sum(dim=1, dtype=torch.float64)[0]
+                            for lo, hi, _ in self.buckets])
+        self._probe_sums.fill_(float("nan"))
+        return [b for b in range(len(self.buckets)) if not bool(got[b] == want[b])]
+
+    def abandon_backward(self) -> None:
+        """A backward raised part-way: forget its ready marks and queued callback."""
+        if self._callback_queued:
+            self._callback_queued = False
+            self.tracker.finalize()
 
     def _finalize_backward(self):
         self._callback_queued = False

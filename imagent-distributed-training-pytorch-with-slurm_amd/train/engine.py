@@ -18,7 +18,6 @@ TensorBoard tags, best-model checkpoint), re-designed for MI355X:
 from __future__ import annotations
 
 import collections
-import faulthandler
 import json
 import math
 import os
@@ -43,6 +42,7 @@ from ..utils.tb import SummaryWriter
 from .lr import Schedule
 from .meters import DeviceMetrics
 from .optim import build_optimizer
+from ..utils.watchdog import maybe_stall
 
 
 class StepRunner:
@@ -53,19 +53,20 @@ class StepRunner:
         self.ddp, self.opt, self.metrics = ddp, opt, metrics
         self.backend, self.smoothing = backend, smoothing
         self.autocast_dtype = autocast_dtype
-        # Run-ahead limit: with no host sync in the step the CPU can queue many steps,
-        # and every queued step keeps its own activations reserved (they are read on the
-        # weight-gradient side stream, so the allocator cannot recycle them before that
-        # stream passes them): measured 252 GiB reserved for a 40.6 GiB peak at R50 / 1024
-        # img, which thrashes the allocator once the GPU is shared. Waiting on the event
-        # of the step `max_inflight` back keeps the GPU fed and the footprint bounded.
+        # Run-ahead limit: with no host sync in the step the CPU can queue many steps, and
+        # every queued step holds its own activations until the step's end-of-backward join
+        # (they are read on the weight-gradient side stream, ops/streams.py): measured 252 GiB
+        # reserved for a 40.6 GiB peak at R50 / 1024 img without a limit, which thrashes the
+        # allocator once the GPU is shared. Waiting (blocking-sync event, no spinning core)
+        # on the step `max_inflight` back keeps the GPU fed and the footprint bounded.
         self.max_inflight = int(os.environ.get("IMAGENT_MAX_INFLIGHT", "2"))
+        self._blocking = os.environ.get("IMAGENT_THROTTLE", "block") == "block"
         self._inflight: collections.deque = collections.deque()
 
     def _throttle(self, dev: torch.device) -> None:
         if self.max_inflight <= 0 or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
             return
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(blocking=self._blocking)  # blocking: the host sleeps, it does not spin
         ev.record(torch.cuda.current_stream(dev))
         self._inflight.append(ev)
         while len(self._inflight) > self.max_inflight:
@@ -88,13 +89,20 @@ class StepRunner:
         return self.ddp(x)
 
     def train_step(self, micro) -> None:
+        from ..ops import streams
+        streams.reset()
         self.opt.zero_grad()
         n = len(micro)
-        for i, (x, y) in enumerate(micro):
-            ctx = self.ddp.no_sync() if i + 1 < n else _null()
-            with ctx:
-                loss = self.loss(self.forward(x), y)
-                (loss / n if n > 1 else loss).backward()
+        try:
+            for i, (x, y) in enumerate(micro):
+                ctx = self.ddp.no_sync() if i + 1 < n else _null()
+                with ctx:
+                    loss = self.loss(self.forward(x), y)
+                    (loss / n if n > 1 else loss).backward()
+        except BaseException:
+            streams.reset()  # a failed backward may have left its join callback unrun
+            self.ddp.abandon_backward()
+            raise
         self.opt.step()
         self._throttle(micro[0][0].device)
 
@@ -148,7 +156,7 @@ class GraphedStep:
         # captured single-stream: capturing the weight-gradient side stream's
         # fork/join (event edges between two streams) segfaults in
         # hipStreamEndCapture on this ROCm 7 / torch 2.10 stack, even with the
-        # join made explicit -- measured, scripts/dev/graph_debug.py
+        # join made explicit -- measured in round 1 (capture experiment)
         overlap = streams.overlap_enabled()
         streams.set_wgrad_overlap(False)
         try:
@@ -167,6 +175,12 @@ class _null:
 
     def __exit__(self, *a):
         return False
+
+
+def _abort_c10d() -> None:
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.distributed_c10d._abort_process_group()
 
 
 def _master_print(is_master, *a, **kw):
@@ -202,10 +216,14 @@ class Trainer:
         ws, rk = self.ctx.world_size, self.ctx.rank
         if a.data == "synthetic":
             self.num_classes = a.num_classes
+            task = getattr(a, "synthetic_task", "random")
+            pool = 4 if task == "random" else 16
             self.train_src = SyntheticImageNet(a.synthetic_train_size, a.image_size, a.num_classes,
-                                               a.batch_size, self.device, a.seed, rank=rk)
+                                               a.batch_size, self.device, a.seed, rank=rk, task=task,
+                                               pool_batches=pool)
             self.val_src = SyntheticImageNet(a.synthetic_val_size, a.image_size, a.num_classes,
-                                             a.batch_size, self.device, a.seed + 1, rank=rk)
+                                             a.batch_size, self.device, a.seed + 1, rank=rk, task=task,
+                                             pool_batches=pool)
             self.n_train, self.n_val = a.synthetic_train_size, a.synthetic_val_size
             self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=a.seed)
             self.val_sampler = ShardSampler(self.n_val, ws, rk, shuffle=True, seed=a.seed)
@@ -300,6 +318,11 @@ class Trainer:
         if self.kernels == "torch" and self.device.type == "cuda" and a.dtype == "bf16":
             ac = torch.bfloat16
         self.step = StepRunner(self.ddp, self.opt, self.metrics, self.kernels, a.label_smoothing, ac)
+        self.watchdog = None
+        if a.step_timeout > 0:
+            from ..utils.watchdog import Watchdog
+            self.watchdog = Watchdog(a.step_timeout, aborts=[self.comm.abort, _abort_c10d],
+                                     label=f"rank {self.ctx.rank}")
         self._graph_step = None
         if getattr(a, "hip_graph", False):
             if self.device.type != "cuda" or self.ctx.world_size > 1:
@@ -356,15 +379,14 @@ class Trainer:
                 continue
             if per_iter:
                 lr = self.sched.apply(self.opt, epoch, it)
-            if a.step_timeout > 0:   # hang detector: dump every thread's stack if a step stalls
-                faulthandler.dump_traceback_later(a.step_timeout, exit=False)
+            if self.watchdog:   # hang detector: no beat for --step-timeout s -> stacks, abort, exit
+                self.watchdog.beat(f"epoch {epoch + 1} step {it}")
+            maybe_stall(self.ctx.rank, it)
             self.timer.mark()
             if graph is not None:
                 graph(*micro[0])
             else:
                 self.step.train_step(micro)
-            if a.step_timeout > 0:
-                faulthandler.cancel_dump_traceback_later()
             if a.check_consistency and (it + 1) % a.check_consistency == 0:
                 self.ddp.check_consistency()
             # one-time bucket rebuild from the observed ready order (iteration 1)
@@ -376,6 +398,8 @@ class Trainer:
             it += 1
             nlog += 1
             if a.log_interval and it % a.log_interval == 0:
+                if not self.comm.healthy():  # asynchronous RCCL error: stop now, not at epoch end
+                    raise RuntimeError("communicator reported an asynchronous error")
                 loss, t1, t5, _ = self.metrics.reduced(self.comm)
                 now = time.time()
                 ips = nlog * a.batch_size * accum * self.ctx.world_size / (now - tlog)
@@ -407,6 +431,8 @@ class Trainer:
         t0 = time.time()
         max_steps = a.max_val_steps if a.max_val_steps > 0 else math.inf
         for i, (x, y) in enumerate(val_loader):
+            if self.watchdog:
+                self.watchdog.beat(f"validation step {i}")
             self.step.eval_step(x, y)
             if i + 1 >= max_steps:
                 break
@@ -459,6 +485,8 @@ class Trainer:
             history.append(dict(epoch=epoch + 1, lr=lr, train_loss=tr_loss, val_loss=va_loss, train_top1=tr1,
                                 val_top1=va1, train_top5=tr5, val_top5=va5, train_time=t_train,
                                 val_time=t_val, img_s=ips))
+            if self.watchdog:
+                self.watchdog.pause()  # checkpoint I/O is not a hang
             if a.checkpoint_dir and self.is_master:
                 ckpt.save_state(os.path.join(a.checkpoint_dir, f"state_{a.arch}.pt"), self.model, self.opt,
                                 epoch, self.best)
@@ -475,6 +503,8 @@ class Trainer:
         return dict(best=self.best, history=history)
 
     def close(self):
+        if self.watchdog:
+            self.watchdog.close()
         if self.tb:
             self.tb.close()
         self.comm.close()

@@ -2,7 +2,7 @@
 
 Usage: python scripts/pmc_summary.py OUT.md FETCH.db WRITE_MFMA.db LDS.db
 
-The three databases are the three passes of scripts/dev/g26.sh (rocprofv3 cannot
+The three databases are three rocprofv3 --pmc passes (see scripts/pmc_passes.sh; rocprofv3 cannot
 collect all counters in one pass).  Counters are joined on kernel name and summed
 over dispatches.  Derived columns (MI355X: 8 XCDs, 256 CUs x 4 SIMDs):
 

@@ -44,3 +44,75 @@ def test_rccl_unavailable_falls_back_on_all_ranks():
     if torch.cuda.is_available():
         pytest.skip("a GPU is present: the RCCL communicator would start")
     mp.start_processes(_worker, args=(_free_port(),), nprocs=2, start_method="spawn", join=True)
+
+
+class _FakeRccl:
+    """Stands in for libimagent_comm: rank 1's ncclCommInitRank fails at once,
+    rank 0's never finishes on its own (it would wait in the RCCL bootstrap for
+    the dead peer) until it is aborted."""
+
+    def __init__(self, rank):
+        self.rank, self.aborted, self.destroyed = rank, False, False
+
+    def imc_unique_id_bytes(self):
+        return 128
+
+    def imc_get_unique_id(self, buf):
+        buf.raw = b"u" * 128
+        return 0
+
+    def imc_comm_init_start(self, uid, n, rank, dev, nev, nb, out):
+        if self.rank == 1:
+            return -2
+        out._obj.value = 0x1000  # a (fake) communicator handle
+        return 0
+
+    def imc_comm_set_stream_mode(self, h, mode):
+        return 0
+
+    def imc_comm_poll(self, h):
+        return -3 if self.aborted else 1
+
+    def imc_abort(self, h):
+        self.aborted = True
+        return 0
+
+    def imc_comm_destroy(self, h):
+        self.destroyed = True
+        return 0
+
+    def imc_last_error(self):
+        return b"simulated init failure on rank 1"
+
+
+def _partial_worker(rank, port, outdir):
+    import os
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        from imagent_amd.ops import _lib
+        from imagent_amd.parallel import comm as C
+        fake = _FakeRccl(rank)
+        _lib.comm = lambda: fake
+        ctx = SimpleNamespace(rank=rank, world_size=2, device=torch.device("cpu"))
+        with pytest.warns(UserWarning, match="own RCCL communicator unavailable"):
+            c = C.make_communicator(ctx, "rccl")
+        assert c.name == "torch"
+        if rank == 0:
+            assert fake.aborted, "rank 0 kept waiting on a communicator its peer abandoned"
+        t = torch.full((4,), float(rank + 1))
+        c.allreduce_(t, "avg")
+        c.join()
+        assert t.tolist() == [1.5] * 4
+        open(os.path.join(outdir, f"ok{rank}"), "w").close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_init_failing_on_one_rank_falls_back_everywhere(tmp_path):
+    """ncclCommInitRank failing on ONE rank must not leave the others
+    blocked in the bootstrap or on a working RCCL communicator."""
+    import os
+    mp.start_processes(_partial_worker, args=(_free_port(), str(tmp_path)), nprocs=2, start_method="spawn",
+                       join=True)
+    assert os.path.exists(tmp_path / "ok0") and os.path.exists(tmp_path / "ok1")

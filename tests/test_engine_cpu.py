@@ -72,3 +72,25 @@ def test_slurm_env_single_task(tmp_path):
                SLURM_NTASKS="1", SLURM_JOB_NODELIST="127.0.0.1")
     out = _run([a for a in COMMON if a != "--quiet-banner"] + ["--epochs", "1", "--tb-dir", ""], tmp_path, env)
     assert "0 - Number of nodes: 1" in out and "0 - Master         : True" in out
+
+
+@pytest.mark.slow
+def test_watchdog_ends_a_hung_two_rank_job(tmp_path):
+    """Rank 1 stalls (fault injection) before step 3; rank 0 then blocks in the
+    gradient all-reduce. With --step-timeout 4 both ranks' watchdogs dump their
+    stacks, abort the communicators and exit non-zero, and the job ends within
+    timeout + a few seconds instead of waiting for the 1800 s collective timeout."""
+    import time
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", IMAGENT_FAULT_STALL="1:3:120")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29533", "-m", "imagent_amd.cli"] + COMMON + \
+          ["--epochs", "1", "--backend", "gloo", "--tb-dir", "", "--step-timeout", "4",
+           "--synthetic-train-size", "160"]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=200)
+    dt = time.monotonic() - t0
+    assert r.returncode != 0, r.stdout[-3000:]
+    assert "[watchdog rank 0] no progress for 4 s" in r.stdout, r.stdout[-3000:]
+    assert "exitcode  : 75" in r.stdout or "exit code 75" in r.stdout or "exitcode: 75" in r.stdout, r.stdout[-2000:]
+    assert dt < 60, dt

@@ -247,8 +247,8 @@ def test_graphed_step_matches_eager():
     # atomic sums (order-nondeterministic, ~1e-7), which now and then move a
     # bf16-rounded activation by one ulp, and BatchNorm affine gradients
     # (sum g*xhat over a random-init network: a small difference of large
-    # sums) amplify that into 1e-3..1e-1 of their update (scripts/dev/
-    # race_hunt.py: bimodal, batch-size dependent, present with every kernel
+    # sums) amplify that into 1e-3..1e-1 of their update (round-1
+    # race hunt: bimodal, batch-size dependent, present with every kernel
     # variant and with the weight-gradient stream off). A broken capture
     # (stale inputs, dropped kernels) moves the update by O(1).
     # (and the random-init network at batch 8 amplifies such flips towards
