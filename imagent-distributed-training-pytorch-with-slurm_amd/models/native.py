@@ -50,7 +50,9 @@ class NativeState:
         self.bnb_fusion = bnb_fusion
         blocks = list(model.blocks())
         for k, b in enumerate(blocks):
-            b._prev_block = blocks[k - 1] if k > 0 else None
+            # a plain reference, NOT a registered submodule (nn.Module.__setattr__ would
+            # nest every earlier block into this one's state_dict / parameters())
+            object.__setattr__(b, "_prev_block", blocks[k - 1] if k > 0 else None)
             b._fuse_bnb = bnb_fusion
             b._last_bn = None
             b._bnb_done = False

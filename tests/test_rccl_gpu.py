@@ -122,7 +122,15 @@ def test_ordering_probe_catches_missing_side_stream_dependency():
         comm.depend_on = lambda stream: None          # the bug under test
         cur = comm._cur
         comm._cur = lambda: torch.cuda.default_stream(comm.device).cuda_stream  # issue from the main stream
-        side = streams.side_stream(torch.device("cuda:0"))
+        # a side stream on a hardware queue of its own (full-CU-mask stream): a stream that
+        # happens to share a queue with the comm stream would serialise the two in hardware
+        # and hide the missing dependency
+        import ctypes as C
+        from imagent_amd.ops import _lib
+        h = C.c_void_p()
+        assert _lib.comm().imc_stream_create(0, 2, C.byref(h)) == 0
+        side = torch.cuda.ExternalStream(h.value, device=torch.device("cuda:0"))
+        streams._streams[0] = side
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             torch.cuda._sleep(200_000_000)  # hold every wgrad of this step back
@@ -132,4 +140,5 @@ def test_ordering_probe_catches_missing_side_stream_dependency():
         comm._cur = cur
         assert len(bad) > 0, "ordering probe did not detect buckets reduced before their wgrad kernels"
     finally:
+        streams._streams.pop(0, None)
         comm.close()
