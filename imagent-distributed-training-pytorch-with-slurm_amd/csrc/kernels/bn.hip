@@ -4,10 +4,11 @@
 // backward and the residual add of torchvision's BasicBlock/Bottleneck
 // (reference model at /root/reference/imagenet.py:312).
 //
-// Statistics: the per-channel (sum, sum of squares) of the BN input come from
-// the producing conv's epilogue (conv_igemm.hip, 32-slot fp32 slab folded by
-// imk_bn_stats_finalize), so the forward is ONE streaming pass: read x
-// (+ residual), write y.
+// Statistics: the per-channel shifted (sum, sum of squares) of the BN input
+// come from the producing conv's epilogue (conv_igemm.hip, 32-slot fp32 slab,
+// shift = the previous batch mean) and imk_bn_stats_finalize turns them into
+// (mean, variance), so the forward is ONE streaming pass: read x (+ residual),
+// write y.
 // Semantics follow nn.BatchNorm2d: biased variance to normalise, unbiased
 // variance into running_var, momentum 0.1, eps 1e-5, num_batches_tracked++.
 //
@@ -101,13 +102,6 @@ __device__ __forceinline__ void st8_q(bf16_t* p, const Vec8& x, uint32_t* q, siz
     }
 }
 
-// mean / invstd from conv-epilogue sums
-__device__ __forceinline__ void mean_rstd(const float* sums, int C, int c, float inv_cnt, float eps,
-                                          float& mean, float& rstd) {
-    mean = sums[c] * inv_cnt;
-    const float var = fmaxf(sums[C + c] * inv_cnt - mean * mean, 0.f);
-    rstd = rsqrtf(var + eps);
-}
 
 // ---------------------------------------------------------------- forward
 // y = relu?( (x-mean)*rstd*g + b  [+ res | + (x2-mean2)*rstd2*g2 + b2] )
@@ -136,14 +130,8 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
         ld8f(b + c0, bb);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            float mean, rstd;
-            if (eval) {  // sums holds running_mean / running_var
-                mean = s0[i];
-                rstd = rsqrtf(s1[i] + eps);
-            } else {
-                mean = s0[i] * inv_cnt;
-                rstd = rsqrtf(fmaxf(s1[i] * inv_cnt - mean * mean, 0.f) + eps);
-            }
+            // training: the finalized batch (mean, biased variance); eval: the running ones
+            const float mean = s0[i], rstd = rsqrtf(s1[i] + eps);
             k[i] = rstd * gg[i];
             o[i] = bb[i] - mean * k[i];
             if (sv && blockIdx.x == 0 && tid < cpr) {
@@ -222,15 +210,35 @@ struct RunDesc {
 __global__ void bn_running_kernel(const RunDesc* __restrict__ d, int n) {
     const RunDesc a = d[blockIdx.x];
     for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-        const float mean = a.sums[c] * a.inv_cnt;
-        const float var = fmaxf(a.sums[a.C + c] * a.inv_cnt - mean * mean, 0.f);
+        const float mean = a.sums[c], var = a.sums[a.C + c];  // finalized (mean, biased variance)
         a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * mean;
         a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * var * a.unbias;
     }
     if (threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
 }
 
-// Fold the conv epilogue's [S][2][C] statistics slab into [2][C] sums.
+// Fold the conv epilogue's [S][2][C] SHIFTED statistics slab (sum d, sum d^2
+// with d = v - shift[c]) into [2][C] = (mean, biased variance), fixed fold order:
+//   mean = shift + E[d],  var = E[d^2] - E[d]^2   (no cancellation when shift ~ mean)
+__global__ __launch_bounds__(64) void stats_finalize_mv_kernel(const float* __restrict__ slab,
+                                                               const float* __restrict__ shift,
+                                                               float* __restrict__ out, int S, int C,
+                                                               float inv_cnt) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= C) return;
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int k = 0; k < S; ++k) {
+        a[k & 3] += slab[(size_t)k * 2 * C + c];
+        b[k & 3] += slab[(size_t)k * 2 * C + C + c];
+    }
+    const float m1 = ((a[0] + a[1]) + (a[2] + a[3])) * inv_cnt;
+    const float m2 = ((b[0] + b[1]) + (b[2] + b[3])) * inv_cnt;
+    out[c] = (shift ? shift[c] : 0.f) + m1;
+    out[C + c] = fmaxf(m2 - m1 * m1, 0.f);
+}
+
+// Fold a [S][n] slab into [n] sums (backward reductions).
 __global__ __launch_bounds__(64) void stats_finalize_kernel(const float* __restrict__ slab,
                                                             float* __restrict__ out, int S, int n) {
     const int i = blockIdx.x * 64 + threadIdx.x;
@@ -527,10 +535,12 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
 
 IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 3) * C; }
 
-IMK_EXPORT int imk_bn_stats_finalize(const float* slab, float* out, int S, int C, void* stream) {
-    const int n2c = 2 * C;
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2c + 63) / 64), dim3(64), 0, (hipStream_t)stream,
-                       slab, out, S, n2c);
+// forward statistics: shifted-sum slab [S][2][C] -> out [2][C] = (mean, biased variance)
+IMK_EXPORT int imk_bn_stats_finalize(const float* slab, const float* shift, float* out, int S, int C, long R,
+                                     void* stream) {
+    if (R <= 0) return -100;
+    hipLaunchKernelGGL(stats_finalize_mv_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                       slab, shift, out, S, C, 1.f / (float)R);
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -80,6 +80,11 @@ struct IGemmArgs {
     // the MFMA as E8M0 scales 127 + e
     const int* xexp;
     const int* wexp;
+    // forward statistics are SHIFTED sums: sum(v - shift[n]), sum((v - shift[n])^2)
+    // with shift = the BN's previous batch mean (null: 0). With shift ~ mean the
+    // variance E[(v-s)^2] - E[v-s]^2 has no catastrophic cancellation even when
+    // |mean| >> std (imk_bn_stats_finalize turns the slab into mean / variance).
+    const float* shift;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
@@ -181,11 +186,14 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
                                               int lane, float* st) {
     const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU, accum = a.flags & IG_ACCUM;
     const int ohw = a.OH * a.OW;
-    float s1[FN][4], s2[FN][4];
+    float s1[FN][4], s2[FN][4], shv[FN][4];
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+        for (int r = 0; r < 4; ++r) {
+            s1[i][r] = s2[i][r] = 0.f;
+            shv[i][r] = (st && a.shift && nb + i * 16 + r < a.Nout) ? a.shift[nb + i * 16 + r] : 0.f;
+        }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
         const int m = mb + j * 16;
@@ -248,8 +256,9 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
             if (st) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    s1[i][r] += v[r];
-                    s2[i][r] += v[r] * v[r];
+                    const float d = v[r] - shv[i][r];
+                    s1[i][r] += d;
+                    s2[i][r] += d * d;
                 }
             }
         }
@@ -430,9 +439,12 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
             }
         }
     }
-    float s1[8], s2[8], s3[8];
+    float s1[8], s2[8], s3[8], shv[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
+    for (int c = 0; c < 8; ++c) {
+        s1[c] = s2[c] = s3[c] = 0.f;
+        shv[c] = (!bnb && st && a.shift && nok) ? a.shift[n + c] : 0.f;
+    }
     const int ohw = a.OH * a.OW;
     constexpr int QB = 4;  // chunks whose global reads are issued together
 #pragma unroll
@@ -511,8 +523,9 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 } else {
 #pragma unroll
                     for (int c = 0; c < 8; ++c) {
-                        s1[c] += v[c];
-                        s2[c] += v[c] * v[c];
+                        const float d = v[c] - shv[c];
+                        s1[c] += d;
+                        s2[c] += d * d;
                     }
                 }
             }

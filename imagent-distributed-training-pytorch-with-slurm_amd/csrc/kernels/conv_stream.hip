@@ -105,9 +105,12 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
         }
     }
-    float s1[8], s2[8], s3[8];
+    float s1[8], s2[8], s3[8], shv[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
+    for (int c = 0; c < 8; ++c) {
+        s1[c] = s2[c] = s3[c] = 0.f;
+        shv[c] = (!bnb && a.stats && a.shift) ? a.shift[n + c] : 0.f;  // shifted forward statistics
+    }
 
     const int ohw = a.OH * a.OW;
     const bool dense = a.sA == 1 && a.H == a.OH && a.W == a.OW;  // input row == output pixel
@@ -277,8 +280,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                         } else {
 #pragma unroll
                             for (int c = 0; c < 8; ++c) {
-                                s1[c] += v[c];
-                                s2[c] += v[c] * v[c];
+                                const float d = v[c] - shv[c];
+                                s1[c] += d;
+                                s2[c] += d * d;
                             }
                         }
                     }

@@ -28,9 +28,9 @@ namespace {
 // Optional BatchNorm(+ReLU) prologue for the stem (BNF): the pool reads the
 // BN INPUT x and pools bf16(relu(x*sc + sh)) -- the BN output (4x the pool's
 // output bytes) is never written or re-read. Per-channel constants from the
-// conv-epilogue sums exactly as bn_fwd_kernel computes them (bn.hip).
+// finalized conv-epilogue statistics exactly as bn_fwd_kernel uses them (bn.hip).
 struct PoolBnf {
-    const float* sums;  // [2][C] sum, sum of squares
+    const float* sums;  // [2][C] mean, biased variance (imk_bn_stats_finalize)
     const float* gamma;
     const float* beta;
     float* save;        // [2][C] mean, rstd (for the backward)
@@ -51,8 +51,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         const int c0 = (int)(t0 % cpr) * 8;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const float mean = bnf.sums[c0 + i] * bnf.inv_cnt;
-            const float rstd = rsqrtf(fmaxf(bnf.sums[C + c0 + i] * bnf.inv_cnt - mean * mean, 0.f) + bnf.eps);
+            const float mean = bnf.sums[c0 + i];  // finalized (mean, biased variance)
+            const float rstd = rsqrtf(bnf.sums[C + c0 + i] + bnf.eps);
             bsc[i] = rstd * bnf.gamma[c0 + i];
             bsh[i] = bnf.beta[c0 + i] - mean * bsc[i];
             if (t0 < cpr) {

@@ -251,7 +251,7 @@ def bind_native(model: ResNet, device, order: Optional[Sequence[int]] = None,
 
 def _conv(x, conv: Conv2d, bn: Optional[BatchNorm2d], train: bool):
     if train:
-        return ConvFn.apply(x, conv.weight, conv, bn.work.slab if bn is not None else None)
+        return ConvFn.apply(x, conv.weight, conv, bn.work if bn is not None else None)
     return igemm_fwd(x, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw,
                      stem=getattr(conv, "stem", False))
 

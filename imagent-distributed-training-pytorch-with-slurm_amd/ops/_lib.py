@@ -86,7 +86,7 @@ class IGemmArgs(C.Structure):
         ("flags", C.c_int),
         ("bnx", C.c_void_p), ("bny", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
         ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
-        ("xexp", C.c_void_p), ("wexp", C.c_void_p),
+        ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p),
     ]
 
 
@@ -139,7 +139,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],
-            "imk_bn_stats_finalize": [vp, vp, i32, i32, vp],
+            "imk_bn_stats_finalize": [vp, vp, vp, i32, i32, i64, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_fwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,

@@ -34,14 +34,14 @@ from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 def _fwd(conv, h, bn):
     return igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw,
-                     stats=bn.work.slab, stem=getattr(conv, "stem", False))
+                     stats=bn.work, stem=getattr(conv, "stem", False))
 
 
 def _fwd8(conv, h, h8, bn):
     """fp8 forward (``Fp8State``) when the input has an e4m3 copy, else bf16."""
     if h8 is None or conv.in_channels % 16:
         return _fwd(conv, h, bn)
-    return igemm_fwd(h8[0], conv.w8, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work.slab,
+    return igemm_fwd(h8[0], conv.w8, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work,
                      fp8=(h8[1], conv.w8_exp))
 
 

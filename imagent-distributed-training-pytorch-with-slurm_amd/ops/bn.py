@@ -1,9 +1,11 @@
 """BatchNorm(+residual add)(+ReLU) on the fused HIP kernels (NHWC bf16).
 
 Training-mode statistics arrive from the producing conv's epilogue as a
-``[STAT_SLOTS, 2, C]`` slab of fp32 partial (sum, sum of squares), folded by
-one tiny launch, so the forward is one streaming pass. ``save`` receives
-(mean, invstd) for the backward.
+``[STAT_SLOTS, 2, C]`` slab of fp32 partial SHIFTED (sum, sum of squares)
+around the previous batch mean (no E[x^2] - mean^2 cancellation when
+|mean| >> std), folded by one tiny launch into (mean, variance), so the
+forward is one streaming pass. ``save`` receives (mean, invstd) for the
+backward and is the next step's shift.
 
 Three forms cover torchvision's blocks (reference model: ``imagenet.py:312``):
   mode 0  y = act(bn(x))                       (conv1/conv2 of a block, stem)
@@ -22,11 +24,14 @@ from . import _lib
 from .grad_sink import notify_ready
 
 
-def stats_finalize(work) -> None:
-    """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab into ``work.stats`` [2, C]."""
+def stats_finalize(work, rows: int) -> None:
+    """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab of shifted sums (around
+    ``work.save[:C]``, the previous batch mean) over ``rows`` values per
+    channel into ``work.stats`` [2, C] = (batch mean, biased variance)."""
     S, _, C = work.slab.shape
-    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.stats.data_ptr(), S, C,
-                                                    _lib.stream_ptr()), "bn stats finalize")
+    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.save.data_ptr(),
+                                                    work.stats.data_ptr(), S, C, rows, _lib.stream_ptr()),
+               "bn stats finalize")
 
 
 def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
@@ -48,9 +53,10 @@ def bn_act_forward(x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2, mode: i
     ``q8`` as in :func:`bn_fwd_launch`."""
     y = torch.empty_like(x)
     w, w2 = bn.work, (bn2.work if bn2 is not None else None)
-    stats_finalize(w)
+    R = x.numel() // x.shape[-1]
+    stats_finalize(w, R)
     if w2 is not None:
-        stats_finalize(w2)
+        stats_finalize(w2, R)
     bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
                   stats2=w2.stats if w2 is not None else None,
                   gamma2=bn2.weight if bn2 is not None else None,

@@ -67,7 +67,10 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
               fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, affine: Optional[torch.Tensor] = None,
               accumulate: bool = False) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
-    per-channel (sum, sumsq) accumulation into ``stats`` [2, Co].
+    per-channel (sum, sumsq) accumulation into ``stats`` (a [STAT_SLOTS, 2, Co]
+    slab), or, given a BatchNorm workspace (``bn.work``), into its slab as
+    sums of ``v - shift`` with shift = that BN's previous batch mean
+    (``work.save[:Co]``; finalize with :func:`ops.bn.stats_finalize`).
 
     ``stem``: x has 4 channels and w is ``[Co][KH][32]`` (row = KW taps x 4
     channels, zero padded) - the row-segment gather of the 7x7 stem.
@@ -102,6 +105,9 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     if bias is not None:
         a.bias = bias.data_ptr()
     if stats is not None:
+        if hasattr(stats, "slab"):  # a BatchNorm's workspace: shifted sums around its last batch mean
+            a.shift = stats.save.data_ptr()
+            stats = stats.slab
         a.stats = stats.data_ptr()
     _lib.check(_lib.kernels().imk_conv_igemm(C.byref(a), tile, _lib.stream_ptr()), "conv fwd")
     return out

@@ -54,7 +54,7 @@ class BNReluPoolFn(torch.autograd.Function):
         y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
         idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
         w = bn.work
-        stats_finalize(w)  # conv-epilogue slab -> sums (also read by the running-stat update)
+        stats_finalize(w, N * H * W)  # conv-epilogue slab -> (mean, var) (also read by the running-stat update)
         _lib.check(_lib.kernels().imk_maxpool_fwd_bn(
             x.data_ptr(), w.stats.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), w.save.data_ptr(),
             y.data_ptr(), idx.data_ptr(), N, H, W, Cc, OH, OW, k, s, p, bn.eps, _lib.stream_ptr()),

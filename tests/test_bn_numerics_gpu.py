@@ -1,0 +1,58 @@
+"""BatchNorm batch statistics when |mean| >> std.
+
+The conv epilogue accumulates per-channel sums of ``v - shift`` and
+``(v - shift)^2`` with shift = the BN's previous batch mean (``work.save``),
+and the finalize kernel returns (mean, biased variance). Raw sum / sum of
+squares in fp32 (E[x^2] - mean^2) loses the variance when |mean|/std ~ 100.
+Reference semantics: ``torch.nn.BatchNorm2d`` training statistics
+(imagenet.py:312); checked against fp64 over the bf16 values the BN reads.
+"""
+
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+DEV = "cuda"
+
+
+def _work(C):
+    from imagent_amd.models.resnet import BNWork
+    from imagent_amd.ops import _lib
+    return BNWork(torch.zeros(_lib.STAT_SLOTS, 2, C, device=DEV), torch.zeros(2, C, device=DEV),
+                  torch.zeros(2, C, device=DEV), torch.zeros(_lib.kernels().imk_bn_bwd_scratch_floats(C), device=DEV))
+
+
+@pytest.mark.parametrize("Co", [64, 256])
+def test_shifted_statistics_large_mean(Co):
+    from imagent_amd.ops.bn import stats_finalize
+    from imagent_amd.ops.conv import igemm_fwd
+    torch.manual_seed(0)
+    N, H, Ci = 1000, 32, 64            # R = 1,024,000 rows per channel
+    x = torch.randn(N, H, H, Ci, device=DEV)
+    x[..., -1] = 1.0                    # a constant input channel carries the large mean
+    w = torch.randn(Co, 1, 1, Ci, device=DEV) * 0.1
+    w[..., -1] = 100.0 + torch.rand(Co, 1, 1, device=DEV)  # mean ~100, std ~0.8: |mean|/std > 100
+    x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    work = _work(Co)
+    R = N * H * H
+    errs = []
+    for call in range(2):
+        work.slab.zero_()
+        y = igemm_fwd(x, w, 1, 0, 1, 1, stats=work)
+        stats_finalize(work, R)
+        yd = y.double().reshape(-1, Co)
+        mean64, var64 = yd.mean(0), yd.var(0, unbiased=False)
+        assert float((mean64.abs() / var64.sqrt()).min()) > 100.0
+        mean, var = work.stats[0].double(), work.stats[1].double()
+        errs.append((float(((mean - mean64).abs() / var64.sqrt()).max()),
+                     float(((var - var64).abs() / var64).max())))
+        work.save[0].copy_(work.stats[0])  # what bn_fwd stores: this batch's mean = next shift
+    # call 0 runs with shift 0 (fresh BN): E[x^2] - mean^2 in fp32 -- printed for contrast only
+    print(f"Co={Co}: shift 0 -> mean err {errs[0][0]:.2e} sd, var rel err {errs[0][1]:.2e}; "
+          f"shifted -> mean err {errs[1][0]:.2e} sd, var rel err {errs[1][1]:.2e}")
+    assert errs[1][0] < 1e-3, errs
+    assert errs[1][1] < 1e-3, errs
