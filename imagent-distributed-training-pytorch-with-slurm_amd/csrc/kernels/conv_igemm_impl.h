@@ -181,91 +181,100 @@ __device__ __forceinline__ void ld4bf(const bf16_t* p, float (&v)[4]) {
 }
 
 // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
+// Channel-fragment outer, pixel inner (as epilogue_bnb): the forward statistics
+// of one fragment column (4 channels: shift, sum, sum of squares) are all that
+// is live, and they go to the slab before the next column.
 template <int FN, int FM>
 __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb,
                                               int lane, float* st) {
     const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU, accum = a.flags & IG_ACCUM;
     const int ohw = a.OH * a.OW;
-    float s1[FN][4], s2[FN][4], shv[FN][4];
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            s1[i][r] = s2[i][r] = 0.f;
-            shv[i][r] = (st && a.shift && nb + i * 16 + r < a.Nout) ? a.shift[nb + i * 16 + r] : 0.f;
-        }
+    long pixo[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
         const int m = mb + j * 16;
-        if (m >= a.M) continue;
         const int img = m / ohw, rem = m - img * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
-        const size_t pix = ((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox;
+        pixo[j] = m < a.M ? (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy : -1;
+    }
+    // shift of fragment column i, software-prefetched one column ahead
+    const bool want_shift = st && a.shift;
+    auto ld_shift = [&](int n, float (&o)[4]) {
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int n = nb + i * 16;
-            if (n >= a.Nout) continue;
-            const bool full = n + 3 < a.Nout && (a.ldy % 4) == 0;
-            float v[4];
+        for (int r = 0; r < 4; ++r) o[r] = (want_shift && n + r < a.Nout) ? a.shift[n + r] : 0.f;
+    };
+    float shn[4];
+    ld_shift(nb, shn);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = acc[i][j][r];
-                if (a.flags & IG_AFFINE) {  // folded inference BN: bias = [scale | shift]
-                    if (n + r < a.Nout) v[r] = fmaf(v[r], a.bias[n + r], a.bias[a.Nout + n + r]);
-                } else if (a.bias) {
-                    v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
-                }
-            }
-            if (out_f32) {
-                float* y = reinterpret_cast<float*>(a.Y) + pix * a.ldy + n;
+    for (int i = 0; i < FN; ++i) {
+        const int n = nb + i * 16;
+        const bool nok = n < a.Nout;
+        const bool full = n + 3 < a.Nout && (a.ldy % 4) == 0;
+        float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+        const float shv[4] = {shn[0], shn[1], shn[2], shn[3]};
+        if (i + 1 < FN) ld_shift(n + 16, shn);
+        if (nok) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (relu) v[r] = fmaxf(v[r], 0.f);
-                if (full) {
-                    *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
-                } else {
-                    for (int r = 0; r < 4; ++r)
-                        if (n + r < a.Nout) y[r] = v[r];
-                }
-            } else {
-                bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pix * a.ldy + n;
-                if (accum) {
-                    if (full) {
-                        const u32x2 o = *reinterpret_cast<const u32x2*>(y);
-                        v[0] += lo_bf(o[0]); v[1] += hi_bf(o[0]); v[2] += lo_bf(o[1]); v[3] += hi_bf(o[1]);
-                    } else {
-                        for (int r = 0; r < 4; ++r)
-                            if (n + r < a.Nout) v[r] += bf2f(y[r]);
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (relu) v[r] = fmaxf(v[r], 0.f);
-                const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
-                if (full) {
-                    *reinterpret_cast<u32x2*>(y) = u32x2{lo, hi};
-                } else {
-                    const bf16_t h[4] = {(bf16_t)(lo & 0xffff), (bf16_t)(lo >> 16), (bf16_t)(hi & 0xffff),
-                                         (bf16_t)(hi >> 16)};
-                    for (int r = 0; r < 4; ++r)
-                        if (n + r < a.Nout) y[r] = h[r];
-                }
-                // statistics of the values BN will actually read (bf16-rounded)
-                v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
-            }
-            if (st) {
+            for (int j = 0; j < FM; ++j) {
+                if (pixo[j] < 0) continue;
+                float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float d = v[r] - shv[i][r];
-                    s1[i][r] += d;
-                    s2[i][r] += d * d;
+                    v[r] = acc[i][j][r];
+                    if (a.flags & IG_AFFINE) {  // folded inference BN: bias = [scale | shift]
+                        if (n + r < a.Nout) v[r] = fmaf(v[r], a.bias[n + r], a.bias[a.Nout + n + r]);
+                    } else if (a.bias) {
+                        v[r] += (n + r < a.Nout) ? a.bias[n + r] : 0.f;
+                    }
+                }
+                if (out_f32) {
+                    float* y = reinterpret_cast<float*>(a.Y) + pixo[j] + n;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (relu) v[r] = fmaxf(v[r], 0.f);
+                    if (full) {
+                        *reinterpret_cast<f32x4*>(y) = f32x4{v[0], v[1], v[2], v[3]};
+                    } else {
+                        for (int r = 0; r < 4; ++r)
+                            if (n + r < a.Nout) y[r] = v[r];
+                    }
+                } else {
+                    bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pixo[j] + n;
+                    if (accum) {
+                        if (full) {
+                            const u32x2 o = *reinterpret_cast<const u32x2*>(y);
+                            v[0] += lo_bf(o[0]); v[1] += hi_bf(o[0]); v[2] += lo_bf(o[1]); v[3] += hi_bf(o[1]);
+                        } else {
+                            for (int r = 0; r < 4; ++r)
+                                if (n + r < a.Nout) v[r] += bf2f(y[r]);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (relu) v[r] = fmaxf(v[r], 0.f);
+                    const uint32_t lo = pack_bf2(v[0], v[1]), hi = pack_bf2(v[2], v[3]);
+                    if (full) {
+                        *reinterpret_cast<u32x2*>(y) = u32x2{lo, hi};
+                    } else {
+                        const bf16_t h[4] = {(bf16_t)(lo & 0xffff), (bf16_t)(lo >> 16), (bf16_t)(hi & 0xffff),
+                                             (bf16_t)(hi >> 16)};
+                        for (int r = 0; r < 4; ++r)
+                            if (n + r < a.Nout) y[r] = h[r];
+                    }
+                    // statistics of the values BN will actually read (bf16-rounded)
+                    v[0] = lo_bf(lo); v[1] = hi_bf(lo); v[2] = lo_bf(hi); v[3] = hi_bf(hi);
+                }
+                if (st) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float d = v[r] - shv[r];
+                        s1[r] += d;
+                        s2[r] += d * d;
+                    }
                 }
             }
         }
-    }
-    if (st) {
-#pragma unroll
-        for (int i = 0; i < FN; ++i) stat_pair_atomic(s1[i], s2[i], st, st + a.Nout, nb + i * 16, a.Nout, lane);
+        if (st) stat_pair_atomic(s1, s2, st, st + a.Nout, n, a.Nout, lane);  // every lane (DPP)
     }
 }
 
@@ -394,6 +403,22 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
     static_assert(NT % CPR == 0 && BM % RG == 0, "epilogue split");
     const bool accum = a.flags & IG_ACCUM, bnb = a.flags & IG_BNBWD;
     const bool has_y = bnb && a.bny, has_x2 = bnb && a.bnx2;
+    // this thread's fixed channel chunk (step 2); the forward-statistics shift is
+    // loaded now so its latency hides behind step (1)
+    const int cc = tid % CPR, rg = tid / CPR;
+    const int n = n0 + cc * 8;
+    const bool nok = n < a.Nout;  // Nout % 8 == 0 on this path
+    float mean[8], rstd[8], sc[8], sh[8], m2[8], r2[8];
+    if (!bnb) {  // forward statistics: mean[] holds the shift (previous batch mean, or 0)
+        const bool ld = st && a.shift && nok;
+        const f32x4 lo = ld ? *reinterpret_cast<const f32x4*>(a.shift + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 hi = ld ? *reinterpret_cast<const f32x4*>(a.shift + n + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            mean[c] = lo[c];
+            mean[4 + c] = hi[c];
+        }
+    }
     // (1) fragments -> LDS (8 B per lane: 4 channels of one pixel)
 #pragma unroll
     for (int j = 0; j < FM; ++j)
@@ -405,10 +430,6 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
         }
     __syncthreads();
     // (2) row chunks: thread -> fixed channel chunk cc, rows rg + RG*q
-    const int cc = tid % CPR, rg = tid / CPR;
-    const int n = n0 + cc * 8;
-    const bool nok = n < a.Nout;  // Nout % 8 == 0 on this path
-    float mean[8], rstd[8], sc[8], sh[8], m2[8], r2[8];
     if (bnb && nok) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -439,12 +460,9 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
             }
         }
     }
-    float s1[8], s2[8], s3[8], shv[8];
+    float s1[8], s2[8], s3[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        s1[c] = s2[c] = s3[c] = 0.f;
-        shv[c] = (!bnb && st && a.shift && nok) ? a.shift[n + c] : 0.f;
-    }
+    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
     const int ohw = a.OH * a.OW;
     constexpr int QB = 4;  // chunks whose global reads are issued together
 #pragma unroll
@@ -523,7 +541,7 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 } else {
 #pragma unroll
                     for (int c = 0; c < 8; ++c) {
-                        const float d = v[c] - shv[c];
+                        const float d = v[c] - mean[c];
                         s1[c] += d;
                         s2[c] += d * d;
                     }

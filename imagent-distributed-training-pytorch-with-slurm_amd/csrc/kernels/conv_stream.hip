@@ -105,12 +105,13 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
         }
     }
-    float s1[8], s2[8], s3[8], shv[8];
+    if (!bnb) {  // forward statistics: mean[] holds the shift (previous batch mean, or 0)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        s1[c] = s2[c] = s3[c] = 0.f;
-        shv[c] = (!bnb && a.stats && a.shift) ? a.shift[n + c] : 0.f;  // shifted forward statistics
+        for (int c = 0; c < 8; ++c) mean[c] = (a.stats && a.shift) ? a.shift[n + c] : 0.f;
     }
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
 
     const int ohw = a.OH * a.OW;
     const bool dense = a.sA == 1 && a.H == a.OH && a.W == a.OW;  // input row == output pixel
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                         } else {
 #pragma unroll
                             for (int c = 0; c < 8; ++c) {
-                                const float d = v[c] - shv[c];
+                                const float d = v[c] - mean[c];
                                 s1[c] += d;
                                 s2[c] += d * d;
                             }

@@ -52,6 +52,8 @@ _EPI_FLAGS = {0: 0, 1: 128, 2: 64}
 # IMAGENT_CONV_STREAM=0: keep short-K 1x1 convs off the streaming kernel
 # (conv_stream.hip) -- A/B switch for benchmarks and numerics tests
 _NOSTREAM = 2048 if os.environ.get("IMAGENT_CONV_STREAM", "1") == "0" else 0
+# IMAGENT_BN_SHIFT=0: forward BN statistics as raw sums (shift 0) -- A/B switch
+_SHIFT = os.environ.get("IMAGENT_BN_SHIFT", "1") != "0"
 
 
 def set_stream(enabled: bool) -> None:
@@ -106,7 +108,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
         a.bias = bias.data_ptr()
     if stats is not None:
         if hasattr(stats, "slab"):  # a BatchNorm's workspace: shifted sums around its last batch mean
-            a.shift = stats.save.data_ptr()
+            if _SHIFT:
+                a.shift = stats.save.data_ptr()
             stats = stats.slab
         a.stats = stats.data_ptr()
     _lib.check(_lib.kernels().imk_conv_igemm(C.byref(a), tile, _lib.stream_ptr()), "conv fwd")
