@@ -91,9 +91,13 @@ def main(argv=None):
                     help="1: capture the whole step in a HIP graph and replay it (1 GPU; launch-bound small batches)")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
                     help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
+                    help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward; fp32: the reference's own "
+                         "precision (imagenet.py:312 trains fp32), PyTorch/MIOpen path only (--kernels torch)")
     a = ap.parse_args(argv)
+    if a.dtype == "fp32" and a.kernels != "torch":
+        raise SystemExit("--dtype fp32 runs on the PyTorch/MIOpen path: add --kernels torch (the HIP kernels are "
+                         "bf16 / fp8 MFMA)")
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and "SLURM_PROCID" not in os.environ:
         raise SystemExit(_self_launch(argv))
 
@@ -169,7 +173,7 @@ def main(argv=None):
             opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=after)
         metrics = DeviceMetrics(dev)
         runner = StepRunner(ddp, opt, metrics, a.kernels, 0.0,
-                            torch.bfloat16 if a.kernels == "torch" else None)
+                            torch.bfloat16 if (a.kernels == "torch" and a.dtype == "bf16") else None)
         if a.kernels == "torch":
             model.to(memory_format=torch.channels_last)
         src = SyntheticImageNet(a.batch_size * 4, a.image_size, 1000, a.batch_size, dev, seed=0,
@@ -219,7 +223,7 @@ def main(argv=None):
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": round(value / base, 3) if base else None,
-                "dtype": ("fp32" if not on_gpu else "bf16" if a.dtype == "bf16" else
+                "dtype": ("fp32" if (not on_gpu or a.dtype == "fp32") else "bf16" if a.dtype == "bf16" else
                           "fp8 (e4m3 forward convs, bf16 backward)"),
                 "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
                         "random-init weights)",

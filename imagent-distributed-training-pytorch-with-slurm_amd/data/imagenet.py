@@ -12,7 +12,9 @@ HIP kernel after a 4x smaller uint8 H2D copy (:mod:`.loader`).
 Index semantics follow torchvision's ImageFolder: classes = sorted wnid
 sub-directories, samples = files of each class in ``sorted(os.walk)`` order
 with the usual image extensions. Human-readable class names come from
-torchvision's ``meta.bin`` (loaded with ``weights_only=True``) when present.
+``meta.bin`` (loaded with ``weights_only=True``), which :mod:`.devkit` writes
+from ``ILSVRC2012_devkit_t12.tar.gz`` while it extracts the archives and
+sorts the flat validation set into class folders, as torchvision does.
 """
 
 from __future__ import annotations
@@ -93,6 +95,8 @@ class ImageNetU8(ImageFolderU8):
     def __init__(self, root: str, split: str = "train", size: Tuple[int, int] = (448, 448)):
         if split not in ("train", "val"):
             raise ValueError(split)
+        from .devkit import prepare
+        prepare(root, split)  # archives / devkit -> <split>/<wnid>/ (torchvision's first-use work)
         super().__init__(os.path.join(root, split), size)
         self.split = split
         self.wnids = list(self.classes)

@@ -46,7 +46,7 @@ def main():
     for n, s, e, st, q in rows:
         by[st].append((s, e))
         sq[st].add(q)
-        names[st][n.split("(")[0].split("<")[0].replace("void ", "").replace("(anonymous namespace)::", "")] += 1
+        names[st][n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]] += 1
     wall = (hi - lo) / nsteps / 1e6
     print(f"{nsteps} steps, wall {wall:.2f} ms/step")
     main_st = max(by, key=lambda k: len(by[k]))

@@ -1,0 +1,71 @@
+"""ILSVRC2012 devkit + archives -> torchvision's ImageNet layout (imagenet.py:293-296).
+
+A synthetic devkit (meta.mat with leaf and non-leaf synsets, validation ground
+truth) and synthetic train / val archives of tiny images; the real files are
+not available here (parity with torchvision's parser: same fields, same
+leaf-only class list, same sorted-file -> ground-truth-line mapping)."""
+
+import io
+import os
+import tarfile
+
+import numpy as np
+import pytest
+
+
+def _tar_add(t, name, data):
+    ti = tarfile.TarInfo(name)
+    ti.size = len(data)
+    t.addfile(ti, io.BytesIO(data))
+
+
+def _png(seed):
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(np.full((6, 6, 3), seed * 20 % 256, dtype=np.uint8)).save(b, format="PNG")
+    return b.getvalue()
+
+
+def _make(root):
+    import scipy.io
+    wnids = ["n01440764", "n01443537", "n01484850"]
+    dt = [("ILSVRC2012_ID", "O"), ("WNID", "O"), ("words", "O"), ("num_children", "O")]
+    syn = np.array([(1, wnids[0], "tench, Tinca tinca", 0), (2, wnids[1], "goldfish, Carassius auratus", 0),
+                    (3, wnids[2], "great white shark", 0), (1001, "n00000001", "fish", 3)], dtype=dt)
+    mat = io.BytesIO()
+    scipy.io.savemat(mat, {"synsets": syn})
+    gt = [2, 1, 3, 2, 1]  # ILSVRC ids of val images 1..5
+    with tarfile.open(os.path.join(root, "ILSVRC2012_devkit_t12.tar.gz"), "w:gz") as t:
+        _tar_add(t, "ILSVRC2012_devkit_t12/data/meta.mat", mat.getvalue())
+        _tar_add(t, "ILSVRC2012_devkit_t12/data/ILSVRC2012_validation_ground_truth.txt",
+                 "\n".join(map(str, gt)).encode())
+    with tarfile.open(os.path.join(root, "ILSVRC2012_img_val.tar"), "w") as t:
+        for i in range(5):
+            _tar_add(t, f"ILSVRC2012_val_{i + 1:08d}.JPEG", _png(i))
+    with tarfile.open(os.path.join(root, "ILSVRC2012_img_train.tar"), "w") as t:
+        for c, w in enumerate(wnids):
+            inner = io.BytesIO()
+            with tarfile.open(fileobj=inner, mode="w") as it:
+                for j in range(2):
+                    _tar_add(it, f"{w}_{j}.JPEG", _png(c * 2 + j))
+            _tar_add(t, f"{w}.tar", inner.getvalue())
+    return wnids, gt
+
+
+def test_devkit_and_archives_give_the_torchvision_layout(tmp_path):
+    pytest.importorskip("scipy")
+    from imagent_amd.data.imagenet import ImageNetU8
+    wnids, gt = _make(str(tmp_path))
+    val = ImageNetU8(str(tmp_path), "val", (6, 6))
+    assert val.wnids == wnids  # 3 leaf classes, the non-leaf synset dropped
+    assert val.classes[0] == ("tench", "Tinca tinca")
+    # image k (sorted file order) carries the class of ground-truth line k
+    got = {os.path.basename(p): y for p, y in val.samples}
+    for k, g in enumerate(gt):
+        assert got[f"ILSVRC2012_val_{k + 1:08d}.JPEG"] == g - 1
+    train = ImageNetU8(str(tmp_path), "train", (6, 6))
+    assert len(train) == 6 and train.targets == [0, 0, 1, 1, 2, 2]
+    x, y = train[3]
+    assert tuple(x.shape) == (6, 6, 3) and y == 1
+    # second construction: layout already in place, nothing re-extracted
+    assert len(ImageNetU8(str(tmp_path), "val", (6, 6))) == 5
