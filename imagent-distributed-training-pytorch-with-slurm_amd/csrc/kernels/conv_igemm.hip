@@ -30,7 +30,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const int bn_hint = tile >= 20 ? 256 >> (tile - 20) : 0;
     if (tile >= 20) tile = 0;
     const bool autotile = tile == 0;
-    if (autotile && a.nth == 1 && a.ntw == 1 && (a.C == 64 || a.C == 128 || a.C == 256)) {
+    if (autotile && a.nth == 1 && a.ntw == 1 && (a.C == 64 || a.C == 128 || a.C == 256 || a.C == 512)) {
         const int r = conv_stream(a, st, bn_hint);
         if (r != 1) return r;
     }

@@ -355,6 +355,17 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
+    // K = 256 / 512 into > 128 channels (bottleneck conv3 / downsample forwards): 64-channel
+    // weight slices resident in LDS, the slices of one pixel range on one XCD (the pixels
+    // are fetched from HBM once and re-read from that XCD's L2). IMAGENT_STREAM_WIDE=0: tiles.
+    static const bool wide = [] {
+        const char* e = getenv("IMAGENT_STREAM_WIDE");
+        return !e || e[0] != '0';
+    }();
+    if (wide && !(a.flags & IG_BNBWD) && (a.C == 256 || a.C == 512) && a.Nout > 128) {
+        if (bn != 0 && bn != 64) return 1;
+        return a.C == 256 ? launch_stream1<256, 64, 2, 0>(a, st) : launch_stream1<512, 64, 1, 0>(a, st);
+    }
     int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (a.flags & IG_BNBWD) {
         // BN-backward epilogue: IMAGENT_STREAM_BNB = 0 (never), 64 / 128 (slice width)
