@@ -4,6 +4,18 @@
 #include "conv_igemm_impl.h"
 
 // Tile selection: Nout <= 64 -> 128x64 (1x4 waves), else 128x128 (2x2 waves).
+// IMAGENT_IGEMM_V2=1: the phased kernel (igemm_dma2_kernel, also explicit tile 10)
+// for the staged-epilogue 256x256 tiles. Measured SLOWER than the single-barrier
+// ring at every R50 shape (256@14 3x3: 426-530 vs 362 us; profiles/
+// r50_conv_phased_kernel.md), so off by default.
+static bool dma2_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("IMAGENT_IGEMM_V2");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const IGemmArgs& a = *args;
     hipStream_t st = (hipStream_t)stream;
@@ -56,6 +68,10 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
+    if (tile == 10) {  // phased 256x256 kernel: staged epilogue only
+        if (!lds_ok) return -105;
+        return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
+    }
     if (bnb || use_lds) {  // the tiles the auto choice makes, with a fused / staged epilogue
         if (regstage || (tile != 2 && tile != 8)) {
             if (tile != 2) tile = 4;
@@ -68,6 +84,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
 #define IG_DB(BM_, BN_, WN_, NS_, NW_, E_)                                                  \
     (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, E_>(a, st)                       \
              : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, E_>(a, st))
+        if (use_lds && tile == 8 && dma2_enabled()) return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
         if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
         return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB

@@ -166,7 +166,7 @@ class RcclCommunicator(Communicator):
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None,
                  key: Optional[str] = None, self_collectives: Optional[bool] = None,
-                 nonblocking: Optional[bool] = None, init_timeout: float = 600.0):
+                 nonblocking: Optional[bool] = None, init_timeout: Optional[float] = None):
         from ..ops import _lib
         self._lib = _lib
         self.L = _lib.comm()
@@ -177,6 +177,8 @@ class RcclCommunicator(Communicator):
             self_collectives = os.environ.get("IMAGENT_RCCL_SELF", "1") != "0"
         if nonblocking is None:
             nonblocking = os.environ.get("IMAGENT_RCCL_NONBLOCKING", "1") != "0"
+        if init_timeout is None:  # a stuck bootstrap falls back to c10d after this long (IMAGENT_RCCL_INIT_TIMEOUT)
+            init_timeout = float(os.environ.get("IMAGENT_RCCL_INIT_TIMEOUT", "180"))
         self.active = world_size > 1 or bool(self_collectives)
         self.collectives = 0  # collectives handed to RCCL so far
         self._held: List[torch.Tensor] = []

@@ -99,11 +99,12 @@ def test_conv_explicit_tiles(tile, shape):
     assert rel(nchw(dx), xr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 2, 4, 8])
+@pytest.mark.parametrize("tile", [0, 2, 4, 8, 10])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 512, 1, 1, 0),
-                                   (5, 96, 7, 64, 1, 1, 0)])
+                                   (5, 96, 7, 64, 1, 1, 0), (2, 64, 8, 256, 1, 1, 0), (3, 128, 15, 320, 3, 1, 1)])
 def test_conv_lds_epilogue(tile, shape):
-    """LDS-staged coalesced epilogue: forward + statistics, dgrad, dgrad accumulate."""
+    """LDS-staged coalesced epilogue: forward + statistics, dgrad, dgrad accumulate
+    (tile 10: the phased 256x256 kernel, 1 to 18 K-tiles, ragged M / N / K)."""
     from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
     N, Ci, H, Co, k, s, p = shape
     torch.manual_seed(4)
