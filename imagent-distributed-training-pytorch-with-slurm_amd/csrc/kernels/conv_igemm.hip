@@ -16,6 +16,15 @@ static bool dma2_enabled() {
     return on;
 }
 
+// IMAGENT_IGEMM_PRIO (A/B): wave priority scheme of the staged-epilogue 256x256 tiles
+static int igemm_prio() {
+    static const int v = [] {
+        const char* e = getenv("IMAGENT_IGEMM_PRIO");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const IGemmArgs& a = *args;
     hipStream_t st = (hipStream_t)stream;
@@ -85,6 +94,12 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, E_>(a, st)                       \
              : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, E_>(a, st))
         if (use_lds && tile == 8 && dma2_enabled()) return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
+        if (use_lds && tile == 8 && igemm_prio() == 1)
+            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 1>(a, st)
+                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 1>(a, st);
+        if (use_lds && tile == 8 && igemm_prio() == 2)
+            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 2>(a, st)
+                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 2>(a, st);
         if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
         return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB

@@ -629,7 +629,10 @@ __device__ __forceinline__ void mfma_stage_fp8(f32x4 (&acc)[FN][FM], const char*
 // EB = operand element bytes: 2 (bf16, 64-deep stages) or 1 (fp8 e4m3, 128-deep
 // stages, IG_FP8): the DMA moves 16-B chunks either way, the gather differs
 // only in elements per chunk.
-template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI, int EB = 2, int FB = 0>  // MODE 0: one tap/stage
+// PRIO (A/B): 1 = s_setprio(1) around each stage's MFMAs, 2 = static priority 1 for the
+// second half of the waves (MI355X_MICROARCH.md "Two waves per SIMD", item 4)
+template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI, int EB = 2, int FB = 0,
+          int PRIO = 0>  // MODE 0: one tap/stage
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -747,6 +750,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     };
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p) issue_next();
+    if (PRIO == 2 && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
     const int fr = lane & 15;
     const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
@@ -768,9 +772,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         if (EB == 1)
             mfma_stage_fp8<FN, FM, FB>(acc, sX + buf * SAB + (wm * TM + fr) * 128, sW + buf * SBB + (wn * TN + fr) * 128,
                                    f8c0, f8c1, sw8, sx8);
-        else
+        else {
+            if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
             mfma_stage<FN, FM>(acc, reinterpret_cast<const bf16_t*>(sX + buf * SAB) + (wm * TM + fr) * LDK,
                                reinterpret_cast<const bf16_t*>(sW + buf * SBB) + (wn * TN + fr) * LDK, fk0, fk1);
+            if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        }
         if (++kt == nk) {
             const int tile = lid + tj * G;
             const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
@@ -1215,16 +1222,16 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0, int PRIO = 0>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     size_t lds = (size_t)NS * (BM + BN) * 128;
     if (EPI == 2) lds = std::max(lds, epi_lds_bytes(BM, BN, NW * 64));
     static int resident = 0;
     if (resident == 0)
-        resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB>, lds, NW * 64);
+        resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, PRIO>, lds, NW * 64);
     const int nk = (a.nth * a.ntw * a.C * EB + 127) / 128;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB>),
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, PRIO>),
                        dim3(EPI == 2 ? ntiles : grid_size(ntiles, nk, resident)), dim3(NW * 64), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
