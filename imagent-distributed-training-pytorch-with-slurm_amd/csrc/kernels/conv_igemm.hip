@@ -20,7 +20,7 @@ static bool dma2_enabled() {
 static int igemm_prio() {
     static const int v = [] {
         const char* e = getenv("IMAGENT_IGEMM_PRIO");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
@@ -94,9 +94,9 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, E_>(a, st)                       \
              : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, E_>(a, st))
         if (use_lds && tile == 8 && dma2_enabled()) return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
-        if (use_lds && tile == 8 && igemm_prio() == 1)
-            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 1>(a, st)
-                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 1>(a, st);
+        if (use_lds && tile == 8 && igemm_prio() == 0)
+            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 0>(a, st)
+                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 0>(a, st);
         if (use_lds && tile == 8 && igemm_prio() == 2)
             return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 2>(a, st)
                            : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 2>(a, st);

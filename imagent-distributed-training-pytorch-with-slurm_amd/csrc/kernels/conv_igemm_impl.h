@@ -100,6 +100,8 @@ struct IGemmArgs {
 #define IG_BF8X 512    // with IG_FP8: the gathered operand X is e5m2 (gradients), Wk e4m3
 #define IG_AFFINE 1024 // inference BN folded into the epilogue: out = acc * bias[n] + bias[Nout + n]
 #define IG_NOSTREAM 2048  // never the streaming short-K 1x1 kernel (conv_stream.hip; A/B testing)
+#define IG_ACCUM_SUB2 4096  // with IG_ACCUM: the old output is valid only at even (y, x) output pixels
+                           // (a stride-2 1x1 dgrad wrote only that parity class, no memset); elsewhere 0
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 static __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes (per TU)
@@ -181,6 +183,12 @@ __device__ __forceinline__ void ld4bf(const bf16_t* p, float (&v)[4]) {
     v[0] = lo_bf(w[0]); v[1] = hi_bf(w[0]); v[2] = lo_bf(w[1]); v[3] = hi_bf(w[1]);
 }
 
+// IG_ACCUM: is the old output at output-grid pixel (oh, ow) valid (see IG_ACCUM_SUB2)?
+__device__ __forceinline__ bool old_valid(const IGemmArgs& a, int oh, int ow) {
+    if (!(a.flags & IG_ACCUM_SUB2)) return true;
+    return (((oh * a.sY + a.oy) | (ow * a.sY + a.ox)) & 1) == 0;
+}
+
 // lane holds channels n = nb + i*16 + (lane>>4)*4 + r (r<4) of pixel m = mb + j*16 + (lane&15)
 // Channel-fragment outer, pixel inner (as epilogue_bnb): the forward statistics
 // of one fragment column (4 channels: shift, sum, sum of squares) are all that
@@ -191,12 +199,14 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
     const bool out_f32 = a.flags & IG_OUT_F32, relu = a.flags & IG_RELU, accum = a.flags & IG_ACCUM;
     const int ohw = a.OH * a.OW;
     long pixo[FM];
+    bool oldok[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
         const int m = mb + j * 16;
         const int img = m / ohw, rem = m - img * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         pixo[j] = m < a.M ? (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy : -1;
+        oldok[j] = accum && old_valid(a, oh, ow);
     }
     // shift of fragment column i, software-prefetched one column ahead
     const bool want_shift = st && a.shift;
@@ -241,7 +251,7 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
                     }
                 } else {
                     bf16_t* y = reinterpret_cast<bf16_t*>(a.Y) + pixo[j] + n;
-                    if (accum) {
+                    if (oldok[j]) {
                         if (full) {
                             const u32x2 o = *reinterpret_cast<const u32x2*>(y);
                             v[0] += lo_bf(o[0]); v[1] += hi_bf(o[0]); v[2] += lo_bf(o[1]); v[3] += hi_bf(o[1]);
@@ -296,12 +306,14 @@ __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&a
     const bool has_y = a.bny != nullptr, has_x2 = a.bnx2 != nullptr;
     const int ohw = a.OH * a.OW;
     long pixo[FM];
+    bool oldok[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
         const int m = mb + j * 16;
         const int img = m / ohw, rem = m - img * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         pixo[j] = m < a.M ? (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy : -1;
+        oldok[j] = accum && old_valid(a, oh, ow);
     }
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -327,7 +339,7 @@ __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&a
             xw[j] = *reinterpret_cast<const u32x2*>(a.bnx + e);
             if (has_y) yw[j] = *reinterpret_cast<const u32x2*>(a.bny + e);
             if (has_x2) x2w[j] = *reinterpret_cast<const u32x2*>(a.bnx2 + e);
-            if (accum) ow[j] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(a.Y) + e);
+            if (oldok[j]) ow[j] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(a.Y) + e);
         }
         float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -479,7 +491,11 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 const int img = m / ohw, rem = m - img * ohw;
                 const int oh = rem / a.OW, ow = rem - oh * a.OW;
                 e[u] = (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy + n;
-                if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
+                if (accum) {
+                    oo[u] = old_valid(a, oh, ow)
+                                ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u])
+                                : u32x4{0u, 0u, 0u, 0u};
+                }
                 if (bnb) {
                     xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
                     if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
@@ -629,10 +645,11 @@ __device__ __forceinline__ void mfma_stage_fp8(f32x4 (&acc)[FN][FM], const char*
 // EB = operand element bytes: 2 (bf16, 64-deep stages) or 1 (fp8 e4m3, 128-deep
 // stages, IG_FP8): the DMA moves 16-B chunks either way, the gather differs
 // only in elements per chunk.
-// PRIO (A/B): 1 = s_setprio(1) around each stage's MFMAs, 2 = static priority 1 for the
-// second half of the waves (MI355X_MICROARCH.md "Two waves per SIMD", item 4)
+// PRIO: 1 (default) = s_setprio(1) around each stage's MFMAs (256@14 3x3 fwd 366 -> 357 us,
+// 512@7 3x3 337 -> 320 us, bench +0.9 %), 0 = none, 2 = static priority 1 for the second half
+// of the waves (MI355X_MICROARCH.md "Two waves per SIMD", item 4: neutral here)
 template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI, int EB = 2, int FB = 0,
-          int PRIO = 0>  // MODE 0: one tap/stage
+          int PRIO = 1>  // MODE 0: one tap/stage
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -1222,7 +1239,7 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0, int PRIO = 0>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0, int PRIO = 1>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     size_t lds = (size_t)NS * (BM + BN) * 128;

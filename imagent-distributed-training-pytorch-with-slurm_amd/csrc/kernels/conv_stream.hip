@@ -187,7 +187,15 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 const int m = g * 16 + u * PPR + lane / CH;
                 e[u] = m < a.M ? (long)m * a.ldy + n : -1;
                 if (e[u] >= 0) {
-                    if (accum) oo[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u]);
+                    if (accum) {
+                        bool ok = true;
+                        if (a.flags & IG_ACCUM_SUB2) {  // dense output grid: (oh, ow) of row m
+                            const int rem = m % ohw, oh = rem / a.OW;
+                            ok = ((oh | (rem - oh * a.OW)) & 1) == 0;
+                        }
+                        oo[u] = ok ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u])
+                                   : u32x4{0u, 0u, 0u, 0u};
+                    }
                     if (bnb) {
                         xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
                         if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);

@@ -26,10 +26,16 @@ It also removes ~6 autograd nodes and their Python dispatch per block.
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
+
+
+# IMAGENT_SPARSE_DS=0: memset the stride-2 downsample dgrad's output (A/B switch)
+_SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 
 
 def _fwd(conv, h, bn):
@@ -120,6 +126,7 @@ class BlockFn(torch.autograd.Function):
         fuse = getattr(block, "_fuse_bnb", False)
         premasked = getattr(block, "_bnb_done", False)
         dA8 = None
+        sparse = False
         if ds is not None:
             if premasked:  # dout already masked + reduced by the next block's conv1 dgrad
                 g8a = q.grad_out(a_last, bn_l) if q is not None else None
@@ -130,8 +137,11 @@ class BlockFn(torch.autograd.Function):
                 dA, dAd = bn_act_backward(dout, a_last, ad, out, bn_l, ds[1], 2, True)
                 dAd8 = None
             dconv = ds[0]
+            # a stride-2 1x1 downsample reaches only the even pixels: write those, no memset of the
+            # rest (conv1's dgrad below accumulates with old_sub2 = zeros at the odd ones)
+            sparse = _SPARSE_DS and dconv.stride == 2 and dconv.kh == 1 and dconv.kw == 1 and dconv.padding == 0
             dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw,
-                             fp8=_dg8(dAd8, dconv))
+                             fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
         elif premasked:
             g8a = q.grad_out(a_last, bn_l) if q is not None else None
@@ -167,7 +177,7 @@ class BlockFn(torch.autograd.Function):
                     pds = prev.downsample
                     fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
-                            accumulate=True, bnb=fz, fp8=_dg8(dA8, conv))
+                            accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
                 conv_wgrad(conv, dA, h_in)
                 if fz is not None:
                     prev._bnb_done = True

@@ -119,7 +119,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
 def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int,
                 KH: int, KW: int, out: Optional[torch.Tensor] = None,
                 accumulate: bool = False, tile: int = 0, bnb: Optional["BNBwdFuse"] = None,
-                epi: int = 0, fp8=None) -> torch.Tensor:
+                epi: int = 0, fp8=None, sparse: bool = False, old_sub2: bool = False) -> torch.Tensor:
     """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci,KH,KW,Co]).
 
     Stride 1: one gather-GEMM launch with the taps mirrored.
@@ -132,6 +132,10 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
     BN's slab (finish with :func:`ops.bn.bn_apply_backward`).
     ``fp8 = (dy8, exp_dy, wt8, exp_w)``: e5m2 gradient x e4m3 transposed
     weights on the block-scaled MFMA (device int32 exponents).
+    ``sparse`` (stride 2, 1x1): write only the computed parity class, no memset
+    of the others -- the caller's next dgrad accumulates with ``old_sub2``.
+    ``old_sub2`` (with ``accumulate``): ``out`` holds valid values only at even
+    (y, x) pixels (a ``sparse`` stride-2 dgrad), zeros elsewhere by definition.
     """
     assert not accumulate or out is not None
     N, OH, OW, Co = dy.shape
@@ -145,7 +149,11 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
     if not accumulate and S > 1 and (KH < S or KW < S):
         # some parity classes get no tap (e.g. a strided 1x1): one memset of
         # the output instead of zero-producing GEMM launches for those classes
-        out.zero_()
+        # (sparse: no memset either; the consumer knows those pixels are zero)
+        if sparse:
+            assert S == 2 and KH == 1 and KW == 1 and pad == 0, "sparse: stride-2 1x1 dgrads only"
+        else:
+            out.zero_()
         skip_empty = True
     else:
         skip_empty = accumulate
@@ -175,7 +183,8 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi] | (256 | 512 if fp8 is not None else 0) | _NOSTREAM
+            a.flags = (8 if accumulate else 0) | _EPI_FLAGS[epi] | (256 | 512 if fp8 is not None else 0) | _NOSTREAM | \
+                (4096 if (accumulate and old_sub2) else 0)
             if bnb is not None:
                 bnb.fill(a)
             _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")

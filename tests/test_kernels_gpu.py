@@ -537,3 +537,26 @@ def test_colsum_accumulates(R, Cc):
     ref = out + x.float().sum(0)
     colsum_into(x, out)
     assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("cmid,cin,tile,epi", [(64, 256, 0, 0), (128, 256, 0, 0), (256, 512, 0, 0),
+                                               (128, 512, 8, 2), (96, 256, 2, 1), (64, 128, 4, 0)])
+def test_sparse_downsample_dgrad_then_accumulate(cmid, cin, tile, epi):
+    """Bottleneck downsample backward without the memset: the stride-2 1x1 dgrad writes only
+    the even pixels (sparse) and conv1's dgrad accumulates treating the odd ones as zero
+    (IG_ACCUM_SUB2) -- bit-identical to memset + dense accumulate, on every epilogue path."""
+    from imagent_amd.ops.conv import igemm_dgrad
+    torch.manual_seed(9)
+    N, H = 3, 14
+    cds = 2 * cin
+    g_ds = bf(torch.randn(N, H // 2, H // 2, cds, device=DEV))
+    w_ds = bf(torch.randn(cin, 1, 1, cds, device=DEV) * 0.05)   # [Ci][KH][KW][Co] (transposed)
+    g1 = bf(torch.randn(N, H, H, cmid, device=DEV))
+    w1 = bf(torch.randn(cin, 1, 1, cmid, device=DEV) * 0.1)
+    ref = igemm_dgrad(g_ds, w_ds, (H, H), 2, 0, 1, 1)                     # memset + class (0, 0)
+    igemm_dgrad(g1, w1, (H, H), 1, 0, 1, 1, out=ref, accumulate=True, tile=tile, epi=epi)
+    got = torch.full_like(ref, float("nan"))                              # garbage where not written
+    igemm_dgrad(g_ds, w_ds, (H, H), 2, 0, 1, 1, out=got, sparse=True)
+    assert torch.isnan(got[:, 1::2].float()).all() and torch.isnan(got[:, :, 1::2].float()).all()
+    igemm_dgrad(g1, w1, (H, H), 1, 0, 1, 1, out=got, accumulate=True, tile=tile, epi=epi, old_sub2=True)
+    assert torch.equal(got, ref)

@@ -92,6 +92,7 @@ def test_ddp_step_over_rccl_orders_buckets_after_wgrad():
             runner.train_step([_batch(step)])
             torch.cuda.synchronize()
             assert streams.held() == 0, "side-stream operands not released at the end-of-backward join"
+            assert len(runner._inflight) <= runner.max_inflight  # run-ahead limit (blocking events)
             bad = ddp.verify_order()  # before the relayout below moves the buckets
             assert bad == [], f"step {step}: buckets {bad} all-reduced before their producers finished"
             # iteration-1 relayout, as Trainer.train_epoch does it
