@@ -197,13 +197,11 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
                     (LDS_PTR(s16x4))(base + row_b * PKC));
                 fx[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             }
-            __builtin_amdgcn_s_setprio(1);  // the MFMA burst outranks the partner wave's staging
 #pragma unroll
             for (int i = 0; i < FN; ++i)
 #pragma unroll
                 for (int j = 0; j < FM; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
         }
         if (st + 1 < nst) store(buf ^ 1);
         __syncthreads();

@@ -40,7 +40,7 @@ from ..parallel.sampler import ShardSampler
 from ..utils import checkpoint as ckpt
 from ..utils.tb import SummaryWriter
 from .lr import Schedule
-from .meters import DeviceMetrics
+from .meters import AverageMeter, DeviceMetrics
 from .optim import build_optimizer
 from ..utils.watchdog import maybe_stall
 
@@ -365,7 +365,9 @@ class Trainer:
         it = 0
         max_steps = a.max_steps if a.max_steps > 0 else math.inf
         data_wait = 0.0  # host time blocked on the input pipeline (quirk Q3: measured AND reported)
+        data_time, batch_time = AverageMeter("data"), AverageMeter("batch")  # imagenet.py:99-100, per log line
         loader_it = iter(train_loader)
+        tb = time.perf_counter()
         graph = self._graph_step if (accum == 1 and not per_iter) else None
         while True:
             tw = time.perf_counter()
@@ -374,6 +376,7 @@ class Trainer:
             except StopIteration:
                 break
             data_wait += time.perf_counter() - tw
+            data_time.update(time.perf_counter() - tw)
             micro.append((x, y))
             if len(micro) < accum:
                 continue
@@ -397,6 +400,9 @@ class Trainer:
             micro = []
             it += 1
             nlog += 1
+            now_b = time.perf_counter()
+            batch_time.update(now_b - tb)  # host-side (the GPU runs up to 2 steps behind)
+            tb = now_b
             if a.log_interval and it % a.log_interval == 0:
                 if not self.comm.healthy():  # asynchronous RCCL error: stop now, not at epoch end
                     raise RuntimeError("communicator reported an asynchronous error")
@@ -405,7 +411,8 @@ class Trainer:
                 ips = nlog * a.batch_size * accum * self.ctx.world_size / (now - tlog)
                 _master_print(self.is_master,
                               f"  epoch {epoch + 1} iter {it}/{len(train_loader) // accum} loss {loss:.4f} "
-                              f"top1 {t1:.2f} top5 {t5:.2f} lr {lr:.4g} {ips:.1f} img/s")
+                              f"top1 {t1:.2f} top5 {t5:.2f} lr {lr:.4g} {ips:.1f} img/s | {batch_time} s "
+                              f"| {data_time} s")
                 tlog, nlog = now, 0
             if it >= max_steps:
                 break

@@ -1,8 +1,9 @@
 """Metric helpers.
 
-* :class:`AverageMeter`, :func:`accuracy`, :func:`reduce_tensor` and
-  :func:`to_python_float` keep the reference's semantics
-  (``imagenet.py:44-94``) for API compatibility.
+* :class:`AverageMeter` (host timings), :func:`accuracy` / :func:`topk_hits`,
+  :func:`reduce_tensor` and :func:`to_python_float` keep the reference's
+  semantics (``imagenet.py:44-94``) and are what the engine uses for host
+  timings, the torch-path accuracy counters and the cross-rank reduction.
 * :class:`DeviceMetrics` is what the engine actually uses: a 4-float device
   accumulator ``[loss_sum, top1_hits, top5_hits, rows]`` filled by the fused
   softmax-xent kernel, all-reduced ONCE per logging interval / epoch instead
@@ -22,55 +23,69 @@ import torch.nn.functional as F
 
 
 class AverageMeter:
-    """Computes and stores the average and current value (imagenet.py:44-60)."""
+    """Running value / count-weighted mean (the reference's meter, imagenet.py:44-60).
 
-    def __init__(self):
+    The engine keeps its host-side timings in these (``batch_time``,
+    ``data_time`` in :meth:`Trainer.train_epoch`); the device-side loss and
+    accuracy live in :class:`DeviceMetrics` instead (no per-step host sync)."""
+
+    __slots__ = ("name", "val", "sum", "count")
+
+    def __init__(self, name: str = ""):
+        self.name = name
         self.reset()
 
-    def reset(self):
-        self.val = 0
-        self.avg = 0
-        self.sum = 0
-        self.count = 0
+    def reset(self) -> None:
+        self.val, self.sum, self.count = 0.0, 0.0, 0
 
-    def update(self, val: float, n: int = 1):
-        self.val = val
-        self.sum += val * n
+    def update(self, val: float, n: int = 1) -> None:
+        self.val = float(val)
+        self.sum += self.val * n
         self.count += n
-        self.avg = self.sum / self.count
+
+    @property
+    def avg(self) -> float:
+        return self.sum / self.count if self.count else 0.0
+
+    def __str__(self) -> str:
+        return f"{self.name} {self.val:.4f} ({self.avg:.4f})"
+
+
+def topk_hits(output: torch.Tensor, target: torch.Tensor, topk: Sequence[int] = (1,)) -> torch.Tensor:
+    """Number of rows whose target is among the top-k logits, one count per k
+    (device tensor, no host sync)."""
+    with torch.no_grad():
+        ranked = output.topk(min(max(topk), output.shape[1]), 1).indices
+        hit = ranked == target.reshape(-1, 1)
+        return torch.stack([hit[:, :k].any(1).float().sum() for k in topk])
 
 
 def accuracy(output: torch.Tensor, target: torch.Tensor, topk: Tuple[int, ...] = (1,)) -> List[torch.Tensor]:
-    """Precision@k in percent (imagenet.py:63-79)."""
-    with torch.no_grad():
-        maxk = max(topk)
-        batch_size = target.size(0)
-        _, pred = output.topk(maxk, 1, True, True)
-        pred = pred.t()
-        correct = pred.eq(target.reshape(1, -1).expand_as(pred))
-        res = []
-        for k in topk:
-            correct_k = correct[:k].reshape(-1).float().sum(0, keepdim=True)
-            res.append(correct_k.mul_(100.0 / batch_size))
-        return res
+    """Precision@k in percent, one 1-element tensor per k (imagenet.py:63-79)."""
+    hits = topk_hits(output, target, topk) * (100.0 / target.size(0))
+    return [h.reshape(1) for h in hits]
 
 
-def reduce_tensor(tensor: torch.Tensor, world_size: int, comm=None) -> torch.Tensor:
-    """Cross-rank mean (imagenet.py:82-87)."""
+def reduce_tensor(tensor: torch.Tensor, world_size: int, comm=None, op: str = "mean") -> torch.Tensor:
+    """Cross-rank mean (imagenet.py:82-87) or sum of a copy of ``tensor``,
+    through our communicator when given (else c10d)."""
     rt = tensor.clone()
-    if comm is not None:
-        comm.allreduce_(rt, "sum")
-        comm.join()
-    elif world_size > 1 and torch.distributed.is_initialized():
-        torch.distributed.all_reduce(rt)
-    rt /= world_size
+    if world_size > 1:
+        if comm is not None:
+            comm.allreduce_(rt, "sum")
+            comm.join()
+        elif torch.distributed.is_initialized():
+            torch.distributed.all_reduce(rt)
+    if op == "mean":
+        rt /= world_size
     return rt
 
 
-def to_python_float(t):
+def to_python_float(t) -> float:
+    """Host float of a 1-element tensor or a plain number / sequence (imagenet.py:90-94)."""
     if hasattr(t, "item"):
-        return t.item()
-    return t[0]
+        return float(t.item())
+    return float(t[0]) if isinstance(t, (list, tuple)) else float(t)
 
 
 class DeviceMetrics:
@@ -89,10 +104,9 @@ class DeviceMetrics:
         """Torch-path update (the HIP path's xent kernel accumulates itself)."""
         with torch.no_grad():
             B = target.numel()
-            top5 = logits.topk(min(5, logits.shape[1]), 1).indices
-            hit = top5 == target[:, None]
-            self.buf += torch.stack([loss.detach().float() * B, hit[:, 0].float().sum(),
-                                     hit.any(1).float().sum(), torch.tensor(float(B), device=self.buf.device)])
+            h1, h5 = topk_hits(logits, target, (1, 5))
+            self.buf += torch.stack([loss.detach().float() * B, h1, h5,
+                                     torch.tensor(float(B), device=self.buf.device)])
         self.batches += 1
 
     def count_batch(self):
@@ -100,10 +114,7 @@ class DeviceMetrics:
 
     def reduced(self, comm=None) -> Tuple[float, float, float, float]:
         """(mean loss, top1 %, top5 %, samples) over all ranks. One collective."""
-        t = self.buf.clone()
-        if comm is not None and comm.world_size > 1:
-            comm.allreduce_(t, "sum")
-            comm.join()
-        loss, t1, t5, n = t.tolist()
+        ws = comm.world_size if comm is not None else 1
+        loss, t1, t5, n = reduce_tensor(self.buf, ws, comm, op="sum").tolist()
         n = max(n, 1.0)
         return loss / n, 100.0 * t1 / n, 100.0 * t5 / n, n
