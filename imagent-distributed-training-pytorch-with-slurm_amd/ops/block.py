@@ -30,6 +30,7 @@ import os
 
 import torch
 
+from . import streams
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
@@ -155,6 +156,7 @@ class BlockFn(torch.autograd.Function):
             dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
         else:
             dA, dX = bn_act_backward(dout, a_last, x, out, bn_l, None, 1, True)  # dX = masked dout
+        streams.flush_deferred()  # the next block's conv1 wgrad, after this memory-bound BN pass
         block._last_bn = None
         block._bnb_done = False
         for i in range(n - 1, -1, -1):
@@ -189,7 +191,10 @@ class BlockFn(torch.autograd.Function):
                     fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
                             accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
-                conv_wgrad(conv, dA, h_in)
+                if _DEFER_WGRAD:  # issued by the previous block's backward after its BN pass
+                    streams.defer(lambda c=conv, g=dA, h=h_in: conv_wgrad(c, g, h))
+                else:
+                    conv_wgrad(conv, dA, h_in)
                 if fz is not None:
                     prev._bnb_done = True
         return dX, None

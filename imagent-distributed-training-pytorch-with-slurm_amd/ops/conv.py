@@ -262,6 +262,7 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        streams.flush_deferred()  # (per-op path / stem conv: nothing may stay queued past here)
         (x,) = ctx.saved_tensors
         mod = ctx.mod
         dy = dy.contiguous()

@@ -77,6 +77,8 @@ class BNReluPoolFn(torch.autograd.Function):
             bn.weight.data_ptr(), bn.bias.data_ptr(), w.scratch.data_ptr(), N, H, W, Cc, OH, OW, k, s, p,
             _lib.stream_ptr()), "maxpool bwd + bn reduce")
         dx, _ = bn_apply_backward(g, x, None, bn, None, 0)
+        from . import streams
+        streams.flush_deferred()  # layer1's conv1 weight gradient, after this BN pass
         return dx, None, None, None, None
 
 

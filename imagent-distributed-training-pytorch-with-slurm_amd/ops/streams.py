@@ -108,6 +108,27 @@ def join_side_into_current() -> None:
 
 
 _join_queued = False
+_deferred: list = []
+
+
+def defer(fn) -> None:
+    """Queue a weight-gradient launch to be issued by the NEXT backward node,
+    after its memory-bound BN pass (so the side stream overlaps that node's
+    dgrad instead). Runs right away when the side stream is off."""
+    if active_side_stream() is None:
+        fn()
+    else:
+        _deferred.append(fn)
+
+
+def flush_deferred() -> None:
+    """Issue the queued weight-gradient launches (in order)."""
+    while _deferred:
+        _deferred.pop(0)()
+
+
+def deferred() -> int:
+    return len(_deferred)
 
 
 def held() -> int:
@@ -121,6 +142,7 @@ def reset() -> None:
     backwards would never queue their own join and ``_keep`` would grow)."""
     global _join_queued
     _join_queued = False
+    _deferred.clear()
     if _keep:
         join_side_into_current()
 

@@ -103,6 +103,8 @@ class StepRunner:
             streams.reset()  # a failed backward may have left its join callback unrun
             self.ddp.abandon_backward()
             raise
+        if streams.deferred():  # a deferred weight gradient nobody issued: a graph without a flush point
+            raise RuntimeError("weight-gradient launches left queued after backward")
         self.opt.step()
         self._throttle(micro[0][0].device)
 
