@@ -11,7 +11,7 @@ the kernel names the auto-dispatch launched are recorded with torch.profiler
 (``gpurun_out/conv_shape_kernels.json``, committed as
 ``profiles/conv_shape_kernels.md``); the set over all shapes must cover the
 conv kernels of the bench's rocprof trace (``BENCH_KERNELS``, from
-``profiles/r50_b1024_v8_kernel_stats.md``).
+``profiles/r50_b1024_v9_kernel_stats.md``).
 Reference ops: torchvision resnet convs (imagenet.py:312, fwd :123, bwd :128).
 """
 
@@ -39,18 +39,27 @@ def _shapes(arch, size, batch):
 
 SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _shapes("resnet18", 448, 128)
 
-# conv kernel templates in the R50 bench trace (profiles/r50_b1024_v8_kernel_stats.md);
+# conv kernel templates in the R50 bench trace (profiles/r50_b1024_v9_kernel_stats.md, all launches);
 # update together with the dispatcher
 BENCH_KERNELS = [
-    "conv_stream_kernel<128, 128, 2, 0, false>", "conv_stream_kernel<224, 64, 2, 0, true>",
-    "conv_stream_kernel<256, 64, 2, 0, false>", "conv_stream_kernel<256, 64, 2, 2, false>",
-    "conv_stream_kernel<64, 128, 3, 1, false>", "conv_stream_kernel<64, 256, 3, 0, false>",
-    "conv_stream_kernel<64, 64, 3, 0, false>", "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0>",
-    "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 2, 2, 0>", "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0>",
-    "igemm_dma_kernel<256, 256, 2, 2, 0, 8, 0, 2, 0>", "igemm_dma_kernel<256, 256, 2, 2, 0, 8, 2, 2, 0>",
-    "igemm_rs_kernel<128, 128, 2, 0, 2>", "igemm_rs_kernel<128, 64, 1, 0, 2>",
-    "wgrad_kernel<128, 128, 2, false, 4, 32>", "wgrad_kernel<128, 128, 2, false, 4, 64>",
-    "wgrad_kernel<64, 128, 1, false, 4, 32>", "wgrad_kernel<64, 128, 1, true, 4, 32>",
+    "conv_stream_kernel<128, 128, 2, 0, false>",
+    "conv_stream_kernel<224, 64, 2, 0, true>",
+    "conv_stream_kernel<256, 64, 2, 0, false>",
+    "conv_stream_kernel<256, 64, 2, 2, false>",
+    "conv_stream_kernel<512, 64, 1, 0, false>",
+    "conv_stream_kernel<64, 128, 3, 1, false>",
+    "conv_stream_kernel<64, 256, 3, 0, false>",
+    "conv_stream_kernel<64, 64, 3, 0, false>",
+    "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0, 1>",
+    "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 2, 2, 0, 1>",
+    "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 1>",
+    "igemm_dma_kernel<256, 256, 2, 2, 0, 8, 2, 2, 0, 1>",
+    "igemm_rs_kernel<128, 128, 2, 0, 2>",
+    "igemm_rs_kernel<128, 64, 1, 0, 2>",
+    "wgrad_kernel<128, 128, 2, false, 4, 32>",
+    "wgrad_kernel<128, 128, 2, false, 4, 64>",
+    "wgrad_kernel<64, 128, 1, false, 4, 32>",
+    "wgrad_kernel<64, 128, 1, true, 4, 32>",
 ]
 
 
