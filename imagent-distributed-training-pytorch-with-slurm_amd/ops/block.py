@@ -40,6 +40,8 @@ from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 # (the two passes sharing HBM slowed the BN pass from 13 to 23 ms/step): measured +1.1 % img/s
 # at R50 / 1024 (12,131 vs 12,001). IMAGENT_DEFER_WGRAD=0: right after the dgrad (A/B switch).
 _DEFER_WGRAD = os.environ.get("IMAGENT_DEFER_WGRAD", "1") != "0"
+# IMAGENT_DS_SIDE=0: the downsample conv's forward on the main stream (A/B switch)
+_DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "1") != "0"
 # IMAGENT_SPARSE_DS=0: memset the stride-2 downsample dgrad's output (A/B switch)
 _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 
@@ -79,6 +81,15 @@ class BlockFn(torch.autograd.Function):
         x8 = q.lookup(x) if q is not None else None
         saved = [x]
         h, h8 = x, x8
+        ds = block.downsample
+        # the downsample conv depends only on x: on the (idle in forward) side stream it
+        # runs beside the main chain's memory-bound BN passes
+        side = streams.side_stream(x.device) if (ds is not None and _DS_SIDE and x.is_cuda) else None
+        ad = None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                ad = _fwd8(ds[0], x, x8, ds[1])
         for conv, bn, _ in pairs[:-1]:
             a = _fwd8(conv, h, h8, bn)
             q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
@@ -87,10 +98,14 @@ class BlockFn(torch.autograd.Function):
             saved += [a, h]
         conv, bn, _ = pairs[-1]
         a = _fwd8(conv, h, h8, bn)
-        ds = block.downsample
         q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
         if ds is not None:
-            ad = _fwd8(ds[0], x, x8, ds[1])
+            if side is not None:
+                cur = torch.cuda.current_stream()
+                cur.wait_stream(side)
+                ad.record_stream(cur)  # allocated on the side stream, read / freed in main order
+            else:
+                ad = _fwd8(ds[0], x, x8, ds[1])
             out = bn_act_forward(a, ad, bn, ds[1], 2, True, q8=q8)
         else:
             ad = None
