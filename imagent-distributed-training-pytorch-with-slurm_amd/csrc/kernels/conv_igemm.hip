@@ -25,6 +25,72 @@ static int igemm_prio() {
     return v;
 }
 
+// Wave-quantisation tail of the one-tile-per-block 256x256 kernel (one block per CU): with
+// T tiles on S CUs the last of ceil(T / S) rounds runs T mod S tiles on an otherwise idle chip
+// (R50 at 1024 img: 784 tiles on 256 CUs = 3 rounds + 16 tiles for every N = 256 conv at 14x14).
+// When that remainder is a small fraction of S, the conv is split at an IMAGE boundary: the
+// first I1 images fill exactly the whole rounds with 256x256 tiles, the remaining images run as
+// 128x128 tiles (4x as many blocks, one quarter of the work each) right after. Every pixel-
+// indexed operand advances by whole images; the statistics slabs accumulate across both
+// launches. IMAGENT_IGEMM_TAIL=0 disables, 1 splits every such conv, 2 only those without a
+// fused BN-backward / accumulating epilogue (the forward convs: in backward the weight-gradient
+// side stream already fills the idle CUs of the last round); IMAGENT_IGEMM_TAIL_FRAC sets the
+// largest remainder fraction that is split (default 0.3).
+static int tail_mode() {
+    static const int m = [] {
+        const char* e = getenv("IMAGENT_IGEMM_TAIL");
+        return e ? atoi(e) : 2;
+    }();
+    return m;
+}
+
+static float tail_frac() {
+    static const float f = [] {
+        const char* g = getenv("IMAGENT_IGEMM_TAIL_FRAC");
+        return g ? (float)atof(g) : 0.3f;
+    }();
+    return f;
+}
+
+static int device_cus() {
+    static const int n = [] {
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        return cus;
+    }();
+    return n;
+}
+
+// images of the main part, or 0 when the conv is not split
+static int tail_split_images(const IGemmArgs& a) {
+    const int mode = tail_mode();
+    const float frac = tail_frac();
+    if (mode == 0 || frac <= 0.f || a.N < 2) return 0;
+    if (mode == 2 && (a.flags & (IG_BNBWD | IG_ACCUM))) return 0;
+    const long ohw = (long)a.OH * a.OW;
+    const long nbn = (a.Nout + 255) / 256;
+    const long tiles = ((a.M + 255) / 256) * nbn;
+    const long S = device_cus();
+    const long full = tiles / S, rem = tiles - full * S;
+    if (full < 1 || rem == 0 || rem > frac * S) return 0;
+    const long mt = full * S / nbn;           // M tiles the whole rounds hold
+    const long i1 = mt * 256 / ohw;           // whole images inside them
+    return (i1 >= 1 && i1 < a.N) ? (int)i1 : 0;
+}
+
+static void advance_images(IGemmArgs& t, const IGemmArgs& a, int i1) {
+    const long xs = (long)a.H * a.W * a.C, ys = (long)a.YH * a.YW * a.ldy;
+    t.N = a.N - i1;
+    t.M = t.N * a.OH * a.OW;
+    t.X = a.X + i1 * xs;
+    t.Y = static_cast<bf16_t*>(a.Y) + i1 * ys;  // staged epilogue: bf16 output only
+    if (a.bnx) t.bnx = a.bnx + i1 * ys;
+    if (a.bny) t.bny = a.bny + i1 * ys;
+    if (a.bnx2) t.bnx2 = a.bnx2 + i1 * ys;
+}
+
 IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const IGemmArgs& a = *args;
     hipStream_t st = (hipStream_t)stream;
@@ -100,6 +166,19 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         if (use_lds && tile == 8 && igemm_prio() == 2)
             return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 2>(a, st)
                            : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 2>(a, st);
+        if (use_lds && tile == 8 && autotile) {
+            const int i1 = tail_split_images(a);
+            if (i1 > 0) {
+                IGemmArgs m = a, t = a;
+                m.N = i1;
+                m.M = i1 * a.OH * a.OW;
+                advance_images(t, a, i1);
+                const int r = md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2>(m, st)
+                                      : launch_dma<256, 256, 2, 2, 1, 8, 2>(m, st);
+                if (r != 0) return r;
+                return md == 0 ? launch_dma<128, 128, 2, 2, 0, 4, 2>(t, st) : launch_dma<128, 128, 2, 2, 1, 4, 2>(t, st);
+            }
+        }
         if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
         return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB
