@@ -230,7 +230,17 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
     if (splits <= 0) {
         // ~3 blocks per CU over 256 CUs (4-wave blocks, 2 resident per CU) or
         // ~2 (8-wave blocks, 1 resident), at least 4 stages per block
-        const int target = NW == 4 ? 768 : 512;
+        static const int tgt_env = [] {
+            const char* e = getenv("IMAGENT_WGRAD_TARGET");
+            return e ? atoi(e) : 0;
+        }();
+        // measured (conv_bench, R50 at 1024 img): the stem and the <= 128-channel 3x3 convs
+        // (few tiles, latency-bound staging) gain from 4-5 blocks per CU (stem 1108 -> 944 us,
+        // 64@56 3x3 630 -> 577, 128@28 3x3 502 -> 461); 1x1 convs lose (more split-K atomics)
+        int target = NW == 4 ? 768 : 512;
+        if (NW == 4 && STEM) target = 1280;
+        else if (NW == 4 && a.KH * a.KW > 1 && a.Ci <= 128) target = 1024;
+        if (tgt_env > 0) target = tgt_env;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));
