@@ -110,6 +110,10 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     }
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
+    if (tile == 0 && a.C == 64 && a.Nout == 64 && a.nth == 3 && a.ntw == 3) {
+        const int r = conv_halo(a, st);
+        if (r != 1) return r;
+    }
     const int md = (a.C % BK) == 0 ? 0 : 1;
     // short-K 1x1 convs (K = C = 64 / 128) are HBM streams: weights resident in
     // LDS, pixel fragments straight from HBM (conv_stream.hip); tiles 20/21/22

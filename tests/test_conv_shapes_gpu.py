@@ -74,7 +74,7 @@ def _kernels(fn):
         out = fn()
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
-    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_kernel"))]
+    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_kernel", "halo3x3"))]
 
 
 def _short(names):

@@ -560,3 +560,37 @@ def test_sparse_downsample_dgrad_then_accumulate(cmid, cin, tile, epi):
     assert torch.isnan(got[:, 1::2].float()).all() and torch.isnan(got[:, :, 1::2].float()).all()
     igemm_dgrad(g1, w1, (H, H), 1, 0, 1, 1, out=got, accumulate=True, tile=tile, epi=epi, old_sub2=True)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("shape", [(3, 64, 56), (2, 64, 112)])
+def test_halo_conv3x3(shape):
+    """64 -> 64 3x3 stride-1 convs run on the halo-tiled kernel (conv_halo.hip):
+    forward with BN statistics, dgrad, accumulating dgrad vs fp32, and the
+    kernel that ran is the halo kernel."""
+    from torch.profiler import ProfilerActivity, profile
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
+    N, C, H = shape
+    torch.manual_seed(3)
+    x = bf(torch.randn(N, C, H, H, device=DEV) + 0.5)
+    w = bf(torch.randn(C, C, 3, 3, device=DEV) * (2.0 / (C * 9)) ** 0.5)
+    xr = x.float().requires_grad_(True)
+    yr = F.conv2d(xr, w.float(), None, 1, 1)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    slab = torch.zeros(32, 2, C, device=DEV)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        y = igemm_fwd(nhwc(x), nhwc(w), 1, 1, 3, 3, stats=slab)
+        wt = w.permute(1, 2, 3, 0).contiguous()
+        dx = igemm_dgrad(nhwc(g), wt, (H, H), 1, 1, 3, 3)
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if "halo3x3_kernel" in e.name]
+    assert len(names) >= 2, [e.name for e in prof.events() if "kernel" in e.name][:8]
+    assert rel(nchw(y), yr) < 1e-2
+    yb = nchw(y).float()
+    st = slab.sum(0)
+    assert rel(st[0], yb.sum((0, 2, 3))) < 1e-3 and rel(st[1], (yb * yb).sum((0, 2, 3))) < 1e-3
+    assert rel(nchw(dx), xr.grad) < 1e-2
+    # accumulate: dx += dgrad again
+    base = dx.clone()
+    igemm_dgrad(nhwc(g), wt, (H, H), 1, 1, 3, 3, out=dx, accumulate=True)
+    assert rel(dx.float() - base.float(), nhwc(xr.grad)) < 2e-2
