@@ -127,8 +127,10 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         q0[j] = (r + 1) * PW + (x + 1);
     }
 
-    // ---- staged epilogue: thread = fixed 8-channel chunk ec of pixels ep0 + 64 k
-    const int ec = tid & 7, ep0 = tid >> 3;
+    // ---- staged epilogue, per wave: the wave's own 32 pixels (groups 2w, 2w+1), lane = fixed
+    // 8-channel chunk ec of pixels 32 w + ep0 + 8 k -- no block barrier between a wave's MFMAs
+    // and its epilogue, so one wave's stores overlap the other waves' MFMAs
+    const int ec = lane & 7, ep0 = 32 * wid + (lane >> 3);
     const bool want_st = a.stats != nullptr;
     const bool accum = a.flags & IG_ACCUM;
     const bool has_y = EPI == 1 && a.bny != nullptr, has_x2 = EPI == 1 && a.bnx2 != nullptr;
@@ -195,7 +197,8 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                 }
             }
             __builtin_amdgcn_s_setprio(0);
-            // lane holds channels kq*4 + i*16 + r of pixel (2w + j)*16 + fr -> bf16 into the staging tile
+            // lane holds channels kq*4 + i*16 + r of pixel (2w + j)*16 + fr -> bf16 into the wave's rows
+            // of the staging tile (written and read back by this wave only: LDS order, no barrier)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -205,15 +208,16 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                         u32x2{pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3])};
                 }
         }
-        __syncthreads();
-        if (dbg == 1) continue;
+        if (!active || dbg == 1) continue;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // coalesced epilogue: the band's output pixels are contiguous in NHWC
         const int img = b / bands_per_img, y0 = (b - img * bands_per_img) * R;
         const size_t m0 = (size_t)(img * a.H + y0) * W;
-#pragma unroll
-        for (int k4 = 0; k4 < (BP + 63) / 64; ++k4) {
-            const int p = ep0 + 64 * k4;
-            if (p >= BP) break;
+#pragma unroll 1
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const int p = ep0 + 8 * k4;
             const size_t e = (m0 + p) * 64 + ec * 8;
             float v[8];
             unpack8(*reinterpret_cast<const u32x4*>(sE + p * HALO_SP + ec * 16), v);

@@ -39,9 +39,11 @@ def _shapes(arch, size, batch):
 
 SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _shapes("resnet18", 448, 128)
 
-# conv kernel templates in the R50 bench trace (profiles/r50_b1024_v9_kernel_stats.md, all launches);
+# conv kernel templates in the R50 bench trace (profiles/r50_b1024_v11_kernel_stats.md, all launches);
 # update together with the dispatcher
 BENCH_KERNELS = [
+    "halo3x3_kernel<56, 4, 0>",
+    "halo3x3_kernel<56, 4, 1>",
     "conv_stream_kernel<128, 128, 2, 0, false>",
     "conv_stream_kernel<224, 64, 2, 0, true>",
     "conv_stream_kernel<256, 64, 2, 0, false>",
