@@ -13,6 +13,8 @@
 //   K13     fc bias gradient -> colsum_bf16
 //   -       bf16 weight shadows: [Co][T][Ci] -> [Ci][T][Co] for dgrad (batched)
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -259,6 +261,130 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
         float* slot = bnr.slab + (size_t)(blockIdx.x & 31) * 3 * C;
         for (int c = threadIdx.x; c < 2 * C; c += 256) atomicAdd(slot + (c / C) * C + c % C, red[c / C][c % C]);
     }
+}
+
+// 3x3 / stride 2 / pad 1 max-pool backward with H = 2 OH, W = 2 OW (the ResNet
+// stem pool), one thread per 2x2 input quad and 8-channel chunk: the quad
+// (2i + a, 2j + b) is covered by exactly the windows (i + {0, 1}, j + {0, 1}),
+// so each window's gradient and argmax are loaded once per quad instead of
+// once per input pixel (4 + 4 loads per 4 pixels instead of 16 + 16). Input
+// pixel (a, b) takes window (i + u, j + v) iff (u == 0 || a == 1) and
+// (v == 0 || b == 1), at window offset (1 + a - 2u) * 3 + (1 + b - 2v).
+template <bool BNR>
+__global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               bf16_t* __restrict__ dx, int N, int C, int OH,
+                                                               int OW, PoolBnr bnr) {
+    const uint32_t cpr = C / 8;
+    const uint32_t total = (uint32_t)N * OH * OW * cpr;
+    const int H = 2 * OH, W = 2 * OW;
+    const int cfix = (int)((blockIdx.x * 256u + threadIdx.x) % cpr) * 8;
+    float mean[8], rstd[8], sc[8], sh[8], sgx[8], sg[8];
+    if constexpr (BNR) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            mean[i] = bnr.save[cfix + i];
+            rstd[i] = bnr.save[C + cfix + i];
+            sc[i] = rstd[i] * bnr.gamma[cfix + i];
+            sh[i] = bnr.beta[cfix + i] - mean[i] * sc[i];
+            sgx[i] = sg[i] = 0.f;
+        }
+    }
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+        const uint32_t q = t / cpr, ch = t - q * cpr;
+        const uint32_t qrow = q / (uint32_t)OW, j = q - qrow * OW;
+        const uint32_t n = qrow / (uint32_t)OH, i = qrow - n * OH;
+        u32x4 g[4];
+        u32x2 ii[4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const bool ok = (int)i + u < OH && (int)j + v < OW;
+                const size_t off = (((size_t)n * OH + i + (ok ? u : 0)) * OW + j + (ok ? v : 0)) * C + ch * 8;
+                g[u * 2 + v] = ok ? *reinterpret_cast<const u32x4*>(dy + off) : u32x4{0u, 0u, 0u, 0u};
+                ii[u * 2 + v] = ok ? *reinterpret_cast<const u32x2*>(idx + off) : u32x2{0xffffffffu, 0xffffffffu};
+            }
+        u32x4 xw[4];
+        if constexpr (BNR) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    xw[a * 2 + b] = *reinterpret_cast<const u32x4*>(
+                        bnr.x + (((size_t)n * H + 2 * i + a) * W + 2 * j + b) * C + ch * 8);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float acc[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int v = 0; v < 2; ++v) {
+                        if ((u == 1 && a == 0) || (v == 1 && b == 0)) continue;
+                        const int want = (1 + a - 2 * u) * 3 + (1 + b - 2 * v);
+                        const u32x4 gg = g[u * 2 + v];
+                        const u32x2 w2 = ii[u * 2 + v];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const uint32_t w = c < 2 ? w2[0] : w2[1];
+                            const int s8 = 16 * (c & 1);
+                            if ((int)((w >> s8) & 0xff) == want) acc[2 * c] += lo_bf(gg[c]);
+                            if ((int)((w >> (s8 + 8)) & 0xff) == want) acc[2 * c + 1] += hi_bf(gg[c]);
+                        }
+                    }
+                if constexpr (BNR) {
+                    const u32x4 x4 = xw[a * 2 + b];
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        const float xv = c & 1 ? hi_bf(x4[c >> 1]) : lo_bf(x4[c >> 1]);
+                        if (!(fmaf(xv, sc[c], sh[c]) > 0.f)) acc[c] = 0.f;
+                        const float gq = bf2f(f2bf(acc[c]));
+                        sg[c] += gq;
+                        sgx[c] += gq * ((xv - mean[c]) * rstd[c]);
+                    }
+                }
+                u32x4 o;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[c] = pack_bf2(acc[2 * c], acc[2 * c + 1]);
+                *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + 2 * i + a) * W + 2 * j + b) * C + ch * 8) = o;
+            }
+    }
+    if constexpr (BNR) {  // as maxpool_bwd_kernel: lane xor-fold, LDS adds, one atomic per channel
+        __shared__ float red[2][2048];
+        const int lane = threadIdx.x & 63;
+        for (int c = threadIdx.x; c < 2 * C; c += 256) red[c / C][c % C] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            for (int o2 = (int)cpr; o2 < 64; o2 <<= 1) {
+                sg[c] += __shfl_xor(sg[c], o2, 64);
+                sgx[c] += __shfl_xor(sgx[c], o2, 64);
+            }
+        __syncthreads();
+        if (lane < (int)cpr) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                atomicAdd(&red[0][cfix + c], sgx[c]);
+                atomicAdd(&red[1][cfix + c], sg[c]);
+            }
+        }
+        __syncthreads();
+        float* slot = bnr.slab + (size_t)(blockIdx.x & 31) * 3 * C;
+        for (int c = threadIdx.x; c < 2 * C; c += 256) atomicAdd(slot + (c / C) * C + c % C, red[c / C][c % C]);
+    }
+}
+
+// IMAGENT_POOL_QUAD=0: the per-pixel backward kernel for the stem pool too (A/B)
+bool pool_quad_ok(int H, int W, int OH, int OW, int k, int s, int p) {
+    static const bool on = [] {
+        const char* e = getenv("IMAGENT_POOL_QUAD");
+        return !e || e[0] != '0';
+    }();
+    return on && k == 3 && s == 2 && p == 1 && H == 2 * OH && W == 2 * OW;
 }
 
 // ------------------------------------------------------------------ avgpool
@@ -526,6 +652,13 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
     if (C % 8) return -100;
     const long total = (long)N * H * W * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
+        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<false>), dim3(stream_grid(total / 4)), dim3(256), 0,
+                           (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
+                           OW, PoolBnr{});
+        IMK_CHECK_LAUNCH();
+        return 0;
+    }
     const dim3 g(stream_grid(total)), b(256);
     if ((k + s - 1) / s <= 2)
         hipLaunchKernelGGL(maxpool_bwd_kernel<2>, g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
@@ -561,6 +694,13 @@ IMK_EXPORT int imk_maxpool_bwd_bnr(const void* dy, const void* idx, void* dx, co
     if (C % 8 || C > 2048 || 256 % (C / 8) || (k + s - 1) / s > 2) return -100;
     const long total = (long)N * H * W * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
+    if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
+        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<true>), dim3(stream_grid(total / 4)), dim3(256), 0,
+                           (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
+                           OW, PoolBnr{(const bf16_t*)x, save, gamma, beta, slab});
+        IMK_CHECK_LAUNCH();
+        return 0;
+    }
     const dim3 g(stream_grid(total)), b(256);
     hipLaunchKernelGGL((maxpool_bwd_kernel<2, true>), g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p,

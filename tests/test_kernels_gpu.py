@@ -493,12 +493,14 @@ def test_conv_fp8_dgrad(shape, accum):
     assert rel(dx, ref) < 1e-2
 
 
-def test_maxpool_bwd_bn_reduce_fused():
-    """imk_maxpool_bwd_bnr: pool backward + ReLU mask from x + BN-backward sums."""
+@pytest.mark.parametrize("H", [30, 31, 56])
+def test_maxpool_bwd_bn_reduce_fused(H):
+    """imk_maxpool_bwd_bnr: pool backward + ReLU mask from x + BN-backward sums
+    (even H: the 2x2-quad kernel of the stem pool; odd H: the per-pixel one)."""
     from imagent_amd.ops import _lib
     from imagent_amd.ops.misc import MaxPoolFn
     torch.manual_seed(7)
-    N, H, C = 4, 30, 64
+    N, C = 4, 64
     x = bf(torch.randn(N, H, H, C, device=DEV))
     mean, rstd = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
     gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.2
