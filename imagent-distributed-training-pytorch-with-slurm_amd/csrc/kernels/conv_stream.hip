@@ -159,6 +159,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 row = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
             }
         }
+        if (a.X2) {  // K = [X | X2], each with C / 2 channels per row
+            const int ldx = a.C / 2;
+            const bf16_t* p1 = a.X + row * ldx + fq * 8;
+            const bf16_t* p2 = a.X2 + row * ldx + fq * 8;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const bf16_t* q = ks * 32 < ldx ? p1 + ks * 32 : p2 + (ks * 32 - ldx);
+                pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(q) : u32x4{0u, 0u, 0u, 0u};
+            }
+            return;
+        }
         const bf16_t* p = a.X + row * a.C + fq * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
@@ -168,6 +179,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     for (int d = 0; d < D; ++d) fetch(d, w0 + d * wstride);
     __syncthreads();  // weight slice visible
 
+    // per-output-channel bias (folded BN backward: W c) of the lane's fixed epilogue channels,
+    // added to the bf16-staged sums (only the X2 path has one)
+    float bias[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bias[c] = a.bias ? a.bias[n + c] : 0.f;
     int aoff[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((ks * 4 + fq) ^ (fr & SWM)) * 16);
@@ -242,8 +258,8 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     float v[8];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        v[2 * k] = lo_bf(t[k]);
-                        v[2 * k + 1] = hi_bf(t[k]);
+                        v[2 * k] = lo_bf(t[k]) + bias[2 * k];
+                        v[2 * k + 1] = hi_bf(t[k]) + bias[2 * k + 1];
                         if (accum) {
                             v[2 * k] += lo_bf(oo[q][k]);
                             v[2 * k + 1] += hi_bf(oo[q][k]);
@@ -359,6 +375,17 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         return launch_stream1<7 * 32, 64, 2, 0, true>(a, st);
     }
     if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
+    if (a.X2) {  // folded BN backward (K = 2 x 256 -> 64 channels): this kernel or an error
+        if (a.C != 512 || a.Nout != 64 || !(a.flags & IG_BNBWD) || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
+            a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.H != a.OH || a.W != a.OW || a.ldy != a.Nout ||
+            a.ldb < a.C || (a.bnx2 && !a.bny))
+            return -110;
+        static const int depth = [] {  // IMAGENT_FOLD_D: pixel groups prefetched per wave (A/B)
+            const char* e = getenv("IMAGENT_FOLD_D");
+            return e ? atoi(e) : 1;  // (2 spills: 256 VGPRs + scratch)
+        }();
+        return depth == 1 ? launch_stream<512, 64, 1>(a, st) : launch_stream<512, 64, 2>(a, st);
+    }
     if (a.bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;

@@ -31,8 +31,9 @@ import os
 import torch
 
 from . import streams
-from .bn import bn_act_backward, bn_act_forward, bn_apply_backward
-from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
+from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_bwd_coef
+from .conv import (BNBwdFuse, bnfold_ok, conv_wgrad, conv_wgrad_bnfold, igemm_dgrad, igemm_dgrad_bnfold,
+                   igemm_fwd)
 
 
 # Issue each weight gradient after the BN-backward pass that follows its dgrad, so the side
@@ -69,6 +70,23 @@ def _dg8(d8, conv):
     if d8 is None or getattr(conv, "wt8", None) is None or conv.out_channels % 16:
         return None
     return (d8[0], d8[1], conv.wt8, conv.w8_exp)
+
+
+class _Folded:
+    """A BatchNorm-backward output dx = A g + B x + Cc kept as (g, x, coef): the
+    consumer conv's dgrad and wgrad take it directly (``ops.bn.bn_bwd_coef``)."""
+
+    __slots__ = ("g", "x", "coef")
+
+    def __init__(self, g, x, coef):
+        self.g, self.x, self.coef = g, x, coef
+
+
+def _wgrad(conv, dA, h):
+    if isinstance(dA, _Folded):
+        conv_wgrad_bnfold(conv, dA.g, dA.x, dA.coef, h)
+    else:
+        conv_wgrad(conv, dA, h)
 
 
 class BlockFn(torch.autograd.Function):
@@ -165,25 +183,33 @@ class BlockFn(torch.autograd.Function):
                              fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
         elif premasked:
-            g8a = q.grad_out(a_last, bn_l) if q is not None else None
-            dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
-            dA8 = _use8(q, g8a)
+            if q is None and fuse and n >= 2 and bnfold_ok(conv_l, dout, BNBwdFuse(acts[-1], pairs[-2][1])):
+                # the last BN's backward folded into conv_l's dgrad / wgrad: no dA pass
+                dA = _Folded(dout, a_last, bn_bwd_coef(bn_l, a_last.numel() // a_last.shape[-1]))
+            else:
+                g8a = q.grad_out(a_last, bn_l) if q is not None else None
+                dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
+                dA8 = _use8(q, g8a)
             dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
         else:
             dA, dX = bn_act_backward(dout, a_last, x, out, bn_l, None, 1, True)  # dX = masked dout
         streams.flush_deferred()  # the next block's conv1 wgrad, after this memory-bound BN pass
         block._last_bn = None
         block._bnb_done = False
+        fold_done = None  # side-stream event after a folded wgrad that reads dout (= dX, accumulated below)
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             h_in = inputs[i]
             if i > 0:
                 bn_prev = pairs[i - 1][1]
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
-                dH = igemm_dgrad(dA, conv.wt_bf16, (h_in.shape[1], h_in.shape[2]), conv.stride, conv.padding,
-                                 conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
+                if isinstance(dA, _Folded):
+                    dH = igemm_dgrad_bnfold(dA.g, dA.x, dA.coef, conv, fz)
+                else:
+                    dH = igemm_dgrad(dA, conv.wt_bf16, (h_in.shape[1], h_in.shape[2]), conv.stride,
+                                     conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
                 if not _DEFER_WGRAD:
-                    conv_wgrad(conv, dA, h_in)
+                    _wgrad(conv, dA, h_in)
                 dA_w = dA
                 if fz is not None:
                     g8a = q.grad_out(acts[i - 1], bn_prev) if q is not None else None
@@ -195,7 +221,12 @@ class BlockFn(torch.autograd.Function):
                 if _DEFER_WGRAD:
                     # issued after the BN-backward pass: the side-stream weight gradient then runs
                     # beside the next (compute-bound) dgrad instead of the memory-bound BN pass
-                    conv_wgrad(conv, dA_w, h_in)
+                    _wgrad(conv, dA_w, h_in)
+                if isinstance(dA_w, _Folded) and dA_w.g.is_cuda:
+                    side = streams.active_side_stream()
+                    if side is not None:  # conv1's dgrad below accumulates into dout: after this read
+                        fold_done = torch.cuda.Event()
+                        fold_done.record(side)
             else:
                 prev = getattr(block, "_prev_block", None)
                 fz = None
@@ -204,6 +235,8 @@ class BlockFn(torch.autograd.Function):
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
                     fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
+                if fold_done is not None:
+                    torch.cuda.current_stream().wait_event(fold_done)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
                             accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
                 if _DEFER_WGRAD:  # issued by the previous block's backward after its BN pass
