@@ -149,11 +149,11 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
         Vec8 v[U], s[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const long r = r0 + u * step;
-            if (r < R) {
-                v[u] = ld8(x + (size_t)r * C + c0);
-                if (MODE != 0) s[u] = ld8(x2 + (size_t)r * C + c0);
-            }
+            // unconditional loads from a clamped row: a guarded load makes hipcc branch
+            // around it and wait vmcnt(0) per row (2 loads in flight instead of 2U)
+            const long r = min(r0 + u * step, R - 1);
+            v[u] = ld8(x + (size_t)r * C + c0);
+            if (MODE != 0) s[u] = ld8(x2 + (size_t)r * C + c0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -304,22 +304,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
             u32x4 yv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const long r = r0 + u * step;
-                if (r < R) {
-                    const size_t off = (size_t)r * C + c0;
-                    g[u] = ld8(dy + off);
-                    xv[u] = ld8(x + off);
-                    if (MODE == 2) x2v[u] = ld8(x2 + off);
-                    if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) g[u].v[i] = xv[u].v[i] = x2v[u].v[i] = 0.f;
-                }
+                // clamped row, unconditional loads (see bn_fwd_kernel); rows past R add 0
+                const size_t off = (size_t)min(r0 + u * step, R - 1) * C + c0;
+                g[u] = ld8(dy + off);
+                xv[u] = ld8(x + off);
+                if (MODE == 2) x2v[u] = ld8(x2 + off);
+                if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const long r = r0 + u * step;
-                if (r < R) relu_mask<MASK>(g[u], yv[u], xv[u], sc, sh);
+                relu_mask<MASK>(g[u], yv[u], xv[u], sc, sh);
+                if (r >= R) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) g[u].v[i] = 0.f;
+                }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     acc[0][i] += g[u].v[i] * (xv[u].v[i] - mean[i]) * rstd[i];
@@ -407,14 +406,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         u32x4 yv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const long r = r0 + u * step;
-            if (r < R) {
-                const size_t off = (size_t)r * C + c0;
-                g[u] = ld8(dy + off);
-                xv[u] = ld8(x + off);
-                if (MODE == 2) x2v[u] = ld8(x2 + off);
-                if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
-            }
+            // clamped row, unconditional loads (see bn_fwd_kernel); rows past R are not stored
+            const size_t off = (size_t)min(r0 + u * step, R - 1) * C + c0;
+            g[u] = ld8(dy + off);
+            xv[u] = ld8(x + off);
+            if (MODE == 2) x2v[u] = ld8(x2 + off);
+            if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {

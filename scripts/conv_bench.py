@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--miopen", action="store_true")
+    ap.add_argument("--blas", action="store_true",
+                    help="also time the plain-GEMM equivalent (torch.matmul -> hipBLASLt) of 1x1 stride-1 convs")
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
     ap.add_argument("--no-stats", action="store_true", help="forward without the fused BN statistics")
@@ -106,6 +108,20 @@ def main():
             t_m = timeit(lambda: F.conv2d(xc, wc, None, s, p))
             line += f" | {t_m:8.1f}"
             r["miopen_fwd_us"] = t_m
+        if a.blas and k == 1 and s == 1 and not stem:
+            x2, w2, dy2 = x.view(-1, Ci), w.view(Co, Ci), dy.view(-1, Co)
+            t_bf = timeit(lambda: torch.matmul(x2, w2.t()))
+            t_bd = timeit(lambda: torch.matmul(dy2, w2))
+            t_bw = timeit(lambda: torch.matmul(dy2.t(), x2))
+            line += (f" | blas fwd {t_bf:7.1f} dgrad {t_bd:7.1f} wgrad {t_bw:7.1f} "
+                     f"({flops / t_bf / 1e6:5.0f}/{flops / t_bd / 1e6:5.0f}/{flops / t_bw / 1e6:5.0f} TF)")
+            r["blas_us"] = (t_bf, t_bd, t_bw)
+            tot["blas_fwd"] += t_bf * cnt
+            tot["blas_dgrad"] += t_bd * cnt
+            tot["blas_wgrad"] += t_bw * cnt
+            tot["hip_1x1_fwd"] += t_f * cnt
+            tot["hip_1x1_dgrad"] += t_d * cnt
+            tot["hip_1x1_wgrad"] += t_w * cnt
         if a.fp8 and not stem and Ci % 16 == 0:
             x8 = x.float().clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
             w8 = w.float().to(torch.float8_e4m3fn).view(torch.uint8)

@@ -57,10 +57,10 @@ BENCH_KERNELS = [
     "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 1>",
     "igemm_dma_kernel<256, 256, 2, 2, 0, 8, 2, 2, 0, 1>",
     "igemm_rs_kernel<128, 128, 2, 0, 2>",
-    "wgrad_kernel<128, 128, 2, false, 4, 32>",
-    "wgrad_kernel<128, 128, 2, false, 4, 64>",
-    "wgrad_kernel<64, 128, 1, false, 4, 32>",
-    "wgrad_kernel<64, 128, 1, true, 4, 32>",
+    "wgrad_kernel<128, 128, 2, false, 4, 32, false>",
+    "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
+    "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
+    "wgrad_kernel<64, 128, 1, true, 4, 32, false>",
 ]
 
 
