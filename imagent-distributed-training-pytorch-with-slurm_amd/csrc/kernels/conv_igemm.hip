@@ -2,6 +2,7 @@
 // Kernels, layout and design notes: conv_igemm_impl.h; fp8: conv_igemm_fp8.hip.
 
 #include "conv_igemm_impl.h"
+#include "conv_pingpong.h"
 
 // Tile selection: Nout <= 64 -> 128x64 (1x4 waves), else 128x128 (2x2 waves).
 // IMAGENT_IGEMM_V2=1: the phased kernel (igemm_dma2_kernel, also explicit tile 10)
@@ -14,6 +15,17 @@ static bool dma2_enabled() {
         return e && e[0] == '1';
     }();
     return on;
+}
+
+// IMAGENT_IGEMM_PP (A/B): the ping-pong 256x256 kernel (conv_pingpong.h) in place of the
+// 2-stage ring for the auto-selected 256x256 tiles with C % 64 == 0: 1 = waves 4-7 staggered
+// by half a phase, 2 = not staggered, 0 = off. Explicit tiles 11 / 12 force it.
+static int igemm_pp() {
+    static const int v = [] {
+        const char* e = getenv("IMAGENT_IGEMM_PP");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
 }
 
 // IMAGENT_IGEMM_PRIO (A/B): wave priority scheme of the staged-epilogue 256x256 tiles
@@ -148,6 +160,10 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
+    if (tile == 11 || tile == 12) {  // ping-pong 256x256 kernel: staged epilogue, C % 64 == 0
+        if (!lds_ok || md != 0) return -105;
+        return tile == 11 ? launch_pp<true>(a, st) : launch_pp<false>(a, st);
+    }
     if (tile == 10) {  // phased 256x256 kernel: staged epilogue only
         if (!lds_ok) return -105;
         return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
@@ -171,6 +187,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         if (use_lds && tile == 8 && igemm_prio() == 2)
             return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 2>(a, st)
                            : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 2>(a, st);
+        const int pp = (use_lds && tile == 8 && autotile && md == 0) ? igemm_pp() : 0;
         if (use_lds && tile == 8 && autotile) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {
@@ -178,12 +195,16 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
                 m.N = i1;
                 m.M = i1 * a.OH * a.OW;
                 advance_images(t, a, i1);
-                const int r = md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2>(m, st)
-                                      : launch_dma<256, 256, 2, 2, 1, 8, 2>(m, st);
+                const int r = pp == 1   ? launch_pp<true>(m, st)
+                              : pp == 2 ? launch_pp<false>(m, st)
+                              : md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2>(m, st)
+                                        : launch_dma<256, 256, 2, 2, 1, 8, 2>(m, st);
                 if (r != 0) return r;
                 return md == 0 ? launch_dma<128, 128, 2, 2, 0, 4, 2>(t, st) : launch_dma<128, 128, 2, 2, 1, 4, 2>(t, st);
             }
         }
+        if (pp == 1) return launch_pp<true>(a, st);
+        if (pp == 2) return launch_pp<false>(a, st);
         if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
         return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB

@@ -129,6 +129,18 @@ def test_conv_lds_epilogue(tile, shape):
     assert rel(acc.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
+@pytest.mark.parametrize("tile", [11, 12])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 1, 0), (2, 64, 8, 256, 1, 1, 0),
+                                   (3, 128, 15, 320, 3, 1, 1), (3, 128, 15, 320, 3, 2, 1), (8, 256, 14, 256, 3, 1, 1),
+                                   (2, 128, 9, 192, 1, 1, 0)])
+def test_conv_pingpong(tile, shape):
+    """Ping-pong 256x256 kernel (conv_pingpong.h; 11 staggered, 12 lockstep): forward +
+    statistics, dgrad (incl. strided parity classes), dgrad accumulate against fp32;
+    1 to 18 K-tiles (odd and even counts: both K-tile buffers and the pipeline tail),
+    ragged M and N, several tiles per conv."""
+    test_conv_lds_epilogue(tile, shape)
+
+
 @pytest.mark.parametrize("splits", [0, 3])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 512, 1, 2, 0),
                                    (2, 128, 7, 256, 3, 1, 1), (5, 96, 13, 136, 1, 1, 0)])
