@@ -294,7 +294,9 @@ class Trainer:
         self.native = None
         if self.kernels == "hip":
             from ..models.native import bind_native
-            self.native = bind_native(model, self.device, order, fp8=a.dtype == "fp8")
+            # IMAGENT_WGRAD_OVERLAP=0: weight gradients on the main stream (A/B and diagnostics)
+            self.native = bind_native(model, self.device, order, fp8=a.dtype == "fp8",
+                                      wgrad_overlap=os.environ.get("IMAGENT_WGRAD_OVERLAP", "1") != "0")
             arena = self.native.arena
         else:
             model.to(self.device)
