@@ -28,8 +28,9 @@ def stats_finalize(work, rows: int) -> None:
     """Fold the conv epilogue's [STAT_SLOTS, 2, C] slab of shifted sums (around
     ``work.save[:C]``, the previous batch mean) over ``rows`` values per
     channel into ``work.stats`` [2, C] = (batch mean, biased variance)."""
+    from .conv import _SHIFT  # IMAGENT_BN_SHIFT=0: the epilogues summed raw values (shift 0)
     S, _, C = work.slab.shape
-    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.save.data_ptr(),
+    _lib.check(_lib.kernels().imk_bn_stats_finalize(work.slab.data_ptr(), work.save.data_ptr() if _SHIFT else None,
                                                     work.stats.data_ptr(), S, C, rows, _lib.stream_ptr()),
                "bn stats finalize")
 

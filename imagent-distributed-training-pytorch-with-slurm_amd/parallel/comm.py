@@ -353,5 +353,7 @@ def make_communicator(ctx, kind: str = "auto") -> Communicator:
             warnings.warn(f"own RCCL communicator unavailable ({e}); using the c10d process group")
             return TorchCommunicator()
     if kind == "torch":
+        if not dist.is_initialized():  # single process without a c10d group: nothing to reduce over
+            return LocalCommunicator()
         return TorchCommunicator()
     return LocalCommunicator()

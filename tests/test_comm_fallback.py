@@ -116,3 +116,18 @@ def test_rccl_init_failing_on_one_rank_falls_back_everywhere(tmp_path):
     mp.start_processes(_partial_worker, args=(_free_port(), str(tmp_path)), nprocs=2, start_method="spawn",
                        join=True)
     assert os.path.exists(tmp_path / "ok0") and os.path.exists(tmp_path / "ok1")
+
+
+def test_torch_override_without_process_group(monkeypatch):
+    """IMAGENT_COMM=torch in a single process with no c10d group (the training CLI at one GPU)
+    gives the local communicator instead of failing in dist.get_rank."""
+    from imagent_amd.parallel.comm import make_communicator
+    assert not dist.is_initialized()
+    monkeypatch.setenv("IMAGENT_COMM", "torch")
+    ctx = SimpleNamespace(rank=0, world_size=1, device=torch.device("cpu"))
+    c = make_communicator(ctx, "auto")
+    assert c.name == "local"
+    t = torch.ones(3)
+    c.allreduce_(t, "avg")
+    c.join()
+    assert t.tolist() == [1.0] * 3

@@ -31,8 +31,8 @@ BASE = ["--arch", "resnet18", "--image-size", "64", "--data", "synthetic", "--sy
         "--tb-dir", ""]
 
 
-def _run(args, cwd, timeout=400):
-    env = dict(os.environ, PYTHONPATH=ROOT)
+def _run(args, cwd, timeout=400, **extra_env):
+    env = dict(os.environ, PYTHONPATH=ROOT, **extra_env)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-u", "-m", "imagent_amd.cli"] + args, cwd=cwd, env=env,
@@ -84,3 +84,13 @@ def test_hip_training_variants_converge(tmp_path, extra):
     assert len(top1) == 2, out[-3000:]
     assert summ[-1][0] < first[0] / 3, (first, summ)   # epoch-2 mean vs the first logged interval
     assert top1[-1] > 90.0, top1
+
+
+def test_bn_shift_off_switch_trains(tmp_path):
+    """IMAGENT_BN_SHIFT=0 (forward BN statistics as raw sums, an A/B switch): the finalize must not
+    add the previous batch mean back (it did: NaN losses from the second step on)."""
+    out = _run(BASE + ["--kernels", "hip", "--epochs", "1", "--synthetic-train-size", str(32 * 40)], tmp_path,
+               IMAGENT_BN_SHIFT="0")
+    first, summ, top1 = _curve(out)
+    assert len(summ) == 1 and all(v == v for v in first) and summ[0][0] == summ[0][0], out[-2000:]
+    assert summ[0][0] < first[0], (first, summ)
