@@ -93,4 +93,4 @@ def test_bn_shift_off_switch_trains(tmp_path):
                IMAGENT_BN_SHIFT="0")
     first, summ, top1 = _curve(out)
     assert len(summ) == 1 and all(v == v for v in first) and summ[0][0] == summ[0][0], out[-2000:]
-    assert summ[0][0] < first[0], (first, summ)
+    assert summ[0][0] < 2.0, (first, summ)  # learning: the epoch mean is below chance level (ln 10 = 2.30)
