@@ -83,10 +83,12 @@ def test_hip_training_converges_saves_and_resumes(tmp_path):
 
 @pytest.mark.parametrize("extra", [["--accum-steps", "2"], ["--dtype", "fp8"]], ids=["accum2", "fp8"])
 def test_hip_training_variants_converge(tmp_path, extra):
-    out = _run(BASE + ["--kernels", "hip", "--epochs", "2"] + extra, tmp_path)
+    out = _run(BASE + WARM + ["--kernels", "hip", "--epochs", "2"] + extra, tmp_path)
     first, summ, top1 = _curve(out)
     assert len(top1) == 2, out[-3000:]
-    assert summ[-1][0] < first[0] / 3, (first, summ)   # epoch-2 mean vs the first logged interval
+    # epoch-2 mean under a third of the chance-level loss ln 10 (the first logged interval is no
+    # reference: some runs have learned most of the task by iteration 10)
+    assert summ[-1][0] < 2.303 / 3, (first, summ)
     assert top1[-1] > 90.0, top1
 
 
