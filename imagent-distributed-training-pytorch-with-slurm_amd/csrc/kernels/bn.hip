@@ -238,6 +238,36 @@ __global__ __launch_bounds__(64) void stats_finalize_mv_kernel(const float* __re
     out[C + c] = fmaxf(m2 - m1 * m1, 0.f);
 }
 
+// stats_finalize_mv + the BatchNorm's per-channel affine: for a BN whose apply + ReLU runs on the
+// consumer conv's operand load (ops/block.py, conv_stream XBN / wgrad XB) this replaces the forward
+// pass: save = (mean, rstd) as bn_fwd_kernel writes it, ss = (gamma * rstd, beta - mean * gamma * rstd)
+__global__ __launch_bounds__(64) void stats_finalize_affine_kernel(const float* __restrict__ slab,
+                                                                   float* __restrict__ save, float* __restrict__ out,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta,
+                                                                   float* __restrict__ ss, int S, int C,
+                                                                   float inv_cnt, float eps, int use_shift) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= C) return;
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int k = 0; k < S; ++k) {
+        a[k & 3] += slab[(size_t)k * 2 * C + c];
+        b[k & 3] += slab[(size_t)k * 2 * C + C + c];
+    }
+    const float m1 = ((a[0] + a[1]) + (a[2] + a[3])) * inv_cnt;
+    const float m2 = ((b[0] + b[1]) + (b[2] + b[3])) * inv_cnt;
+    const float mean = (use_shift ? save[c] : 0.f) + m1;  // shift = the previous batch mean (read first)
+    const float var = fmaxf(m2 - m1 * m1, 0.f);
+    out[c] = mean;
+    out[C + c] = var;
+    const float rstd = rsqrtf(var + eps), sc = gamma[c] * rstd;
+    save[c] = mean;
+    save[C + c] = rstd;
+    ss[c] = sc;
+    ss[C + c] = beta[c] - mean * sc;
+}
+
 // Fold a [S][n] slab into [n] sums (backward reductions).
 __global__ __launch_bounds__(64) void stats_finalize_kernel(const float* __restrict__ slab,
                                                             float* __restrict__ out, int S, int n) {
@@ -607,6 +637,16 @@ IMK_EXPORT int imk_bn_stats_finalize(const float* slab, const float* shift, floa
     if (R <= 0) return -100;
     hipLaunchKernelGGL(stats_finalize_mv_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream,
                        slab, shift, out, S, C, 1.f / (float)R);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_finalize_affine(const float* slab, float* save, float* out, const float* gamma,
+                                      const float* beta, float* ss, int S, int C, long R, float eps, int use_shift,
+                                      void* stream) {
+    if (R <= 0) return -100;
+    hipLaunchKernelGGL(stats_finalize_affine_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, slab,
+                       save, out, gamma, beta, ss, S, C, 1.f / (float)R, eps, use_shift);
     IMK_CHECK_LAUNCH();
     return 0;
 }

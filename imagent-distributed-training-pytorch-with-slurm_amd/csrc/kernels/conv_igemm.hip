@@ -120,6 +120,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
         return launch_rs<128, 64, 1, 2>(a, st);
     }
+    if (a.xbn) return (a.flags & (IG_FP8 | IG_OUT_F32 | IG_RELU | IG_AFFINE | IG_STEM)) ? -120 : conv_stream(a, st);
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
     if (a.X2) return conv_stream(a, st);  // folded BN backward: the streaming kernel only
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps

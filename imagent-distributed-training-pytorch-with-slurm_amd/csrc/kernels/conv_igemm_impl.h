@@ -90,6 +90,10 @@ struct IGemmArgs {
     // a BatchNorm backward folded into this dgrad (dgrad(A g + B x + c) = dgrad_{W A}(g) +
     // dgrad_{W B}(x) + W c, ops/conv.py igemm_dgrad_bnfold), with `bias` = W c added to the sums
     const bf16_t* X2;
+    // conv_stream only: the gathered operand is relu(X * xbn[c] + xbn[C + c]) per input channel c --
+    // the producing BatchNorm's apply + ReLU done on the consumer's operand load (ops/block.py),
+    // so the BN output is never written
+    const float* xbn;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)

@@ -40,7 +40,9 @@ namespace {
 // kernel row = 8 taps x 4 channels = 32 K elements, K = KH x 32): one MFMA
 // k-step per kernel row, the lane's B fragment = 2 taps x 4 channels = two
 // 8-B loads (each predicated on the image border).
-template <int K, int BN, int D, int MODE, bool STEM = false>
+// XBN: the pixel operand is relu(x * scale[c] + shift[c]) (a.xbn [2][C]), applied to each B fragment
+// in registers right before its MFMAs (8 channels per lane per k-step: 2 KS x 8 constants per lane)
+template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) {
     constexpr int KS = K / 32;        // MFMA k-steps per group
     constexpr int FN = BN / 16;       // channel fragments
@@ -187,6 +189,21 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     int aoff[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((ks * 4 + fq) ^ (fr & SWM)) * 16);
+    float xsc[XBN ? KS : 1][8], xsh[XBN ? KS : 1][8];  // this lane's channels ks * 32 + fq * 8 + e
+    if constexpr (XBN) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const f32x4 sc4 = *reinterpret_cast<const f32x4*>(a.xbn + ks * 32 + fq * 8 + 4 * h);
+                const f32x4 sh4 = *reinterpret_cast<const f32x4*>(a.xbn + a.C + ks * 32 + fq * 8 + 4 * h);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    xsc[ks][4 * h + r] = sc4[r];
+                    xsh[ks][4 * h + r] = sh4[r];
+                }
+            }
+    }
 
     for (int g0 = w0; g0 < ngroups; g0 += D * wstride) {
 #pragma unroll
@@ -195,7 +212,18 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             if (g >= ngroups) break;
             bf16x8 fb[KS];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) fb[ks] = __builtin_bit_cast(bf16x8, pf[d][ks]);
+            for (int ks = 0; ks < KS; ++ks) {
+                if constexpr (XBN) {  // BN apply + ReLU on the operand (rows past M are never stored)
+                    u32x4 w = pf[d][ks];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        w[k] = pack_bf2(fmaxf(fmaf(lo_bf(w[k]), xsc[ks][2 * k], xsh[ks][2 * k]), 0.f),
+                                        fmaxf(fmaf(hi_bf(w[k]), xsc[ks][2 * k + 1], xsh[ks][2 * k + 1]), 0.f));
+                    fb[ks] = __builtin_bit_cast(bf16x8, w);
+                } else {
+                    fb[ks] = __builtin_bit_cast(bf16x8, pf[d][ks]);
+                }
+            }
             fetch(d, g + D * wstride);
             long e[NR];
             u32x4 oo[NR], xo[NR], yo[NR], x2o[NR];
@@ -337,17 +365,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     }
 }
 
-template <int K, int BN, int D, int MODE, bool STEM = false>
+template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false>
 int launch_stream1(const IGemmArgs& a, hipStream_t st) {
     constexpr int RP = STEM ? 32 : K / 8;
     const size_t lds = (size_t)BN * RP * 16 + 4 * 16 * (BN * 2 + 16);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM>, lds);
+    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM, XBN>, lds);
     const int nsl = a.Nout / BN;
     const int ngroups = (a.M + 15) / 16;
     // enough pixel blocks to fill the chip, but >= D groups per wave
     const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
-    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM>), dim3(npb * nsl), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM, XBN>), dim3(npb * nsl), dim3(256), lds, st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -385,6 +413,16 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
             return e ? atoi(e) : 1;  // (2 spills: 256 VGPRs + scratch)
         }();
         return depth == 1 ? launch_stream<512, 64, 1>(a, st) : launch_stream<512, 64, 2>(a, st);
+    }
+    if (a.xbn) {  // BN apply + ReLU on the operand load: K = 64 / 128 plain-epilogue 1x1 convs only
+        if ((a.flags & (IG_BNBWD | IG_ACCUM)) || a.bias || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
+            a.H != a.OH || a.W != a.OW || a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout ||
+            a.ldb < a.C || a.dh0 != 0 || a.dw0 != 0)
+            return -120;
+        if (a.C == 64 && a.Nout % 256 == 0) return launch_stream1<64, 256, 3, 0, false, true>(a, st);
+        if (a.C == 64 && a.Nout % 128 == 0) return launch_stream1<64, 128, 3, 0, false, true>(a, st);
+        if (a.C == 128 && a.Nout % 128 == 0) return launch_stream1<128, 128, 2, 0, false, true>(a, st);
+        return -120;
     }
     if (a.bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;

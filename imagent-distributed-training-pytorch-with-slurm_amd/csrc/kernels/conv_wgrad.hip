@@ -40,6 +40,9 @@ struct WgradArgs {
     // gradient g and the operand is A g + B x + Cc per channel, x = dYx, coef = [3][Co] (A, B, Cc)
     const bf16_t* dYx;
     const float* dYcoef;
+    // the X operand is relu(X * xbn[c] + xbn[Ci + c]) (BatchNorm apply + ReLU of the conv's input,
+    // never materialised: ops/block.py); 1x1 convs
+    const float* xbn;
 };
 
 namespace {
@@ -53,7 +56,8 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
 // half the operand bytes per MFMA FLOP of a 128x128 tile)
 // BR: pixels (reduction rows) per stage -- 64, or 32 (half the LDS: three
 // 4-wave blocks per CU instead of two, more waves to hide the load latency)
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false>
+// XB: the X operand gets the BatchNorm apply + ReLU of a.xbn while it is staged (1x1 convs)
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false, bool XB = false>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgrad_kernel(const WgradArgs a) {
     constexpr int NT = NW * 64;
     constexpr int WKC = NW / WCO;
@@ -115,6 +119,17 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
             xc[k] = a.dYcoef[2 * a.Co + c];
         }
     }
+    // XB: this thread's 8 X channels are fixed (xci): their BN scale / shift stay in registers
+    float bsc[8], bsh[8];
+    if (XB) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = xk_ok ? xci + k : 0;
+            bsc[k] = a.xbn[c];
+            bsh[k] = a.xbn[a.Ci + c];
+        }
+    }
+    bool xok[XB ? X_CH : 1];  // XB: the row exists (padding rows stay 0, not relu(shift))
     u32x4 rd[D_CH], rx[X_CH], rdx[XF ? D_CH : 1];
     bool rok[XF ? D_CH : 1];  // XF: the row exists (padding rows must contribute 0, not Cc)
     auto load = [&](int st) {
@@ -139,6 +154,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
             const int row = (tid + NT * i) / CPR_X;
             const int m = mb + row;
             u32x4 v = {0, 0, 0, 0};
+            if (XB) xok[i] = false;
             if (m < mend && xk_ok) {
                 const uint32_t img = fdiv((uint32_t)m, a.mg_ohw, a.sh_ohw);
                 const uint32_t rem = (uint32_t)m - img * (uint32_t)(a.OH * a.OW);
@@ -156,6 +172,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
                     }
                 } else if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
                     v = *reinterpret_cast<const u32x4*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.Ci + xci);
+                    if (XB) xok[i] = true;
                 }
             }
             rx[i] = v;
@@ -182,7 +199,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
 #pragma unroll
         for (int i = 0; i < X_CH; ++i) {
             const int id = tid + NT * i;
-            *reinterpret_cast<u32x4*>(x + (id / CPR_X) * PKC + (id % CPR_X) * 16) = rx[i];
+            u32x4 v = rx[i];
+            if (XB) {  // y = relu(x * scale + shift), rounded to bf16 as the BN pass would have stored it
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = xok[i] ? pack_bf2(fmaxf(fmaf(lo_bf(rx[i][k]), bsc[2 * k], bsh[2 * k]), 0.f),
+                                             fmaxf(fmaf(hi_bf(rx[i][k]), bsc[2 * k + 1], bsh[2 * k + 1]), 0.f))
+                                  : 0u;
+            }
+            *reinterpret_cast<u32x4*>(x + (id / CPR_X) * PKC + (id % CPR_X) * 16) = v;
         }
     };
 
@@ -264,7 +289,7 @@ int xf_target() {  // IMAGENT_WGRAD_XF_TARGET: blocks of a folded-BN wgrad (0: t
     return t;
 }
 
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false>
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false, bool XB = false>
 int launch1(WgradArgs a, int splits, hipStream_t st) {
     const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
@@ -294,8 +319,8 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
-    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR, XF>), dim3(ntiles * splits), dim3(NW * 64), lds, st,
-                       a);
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR, XF, XB>), dim3(ntiles * splits), dim3(NW * 64), lds,
+                       st, a);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -314,6 +339,9 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
     if constexpr (!STEM) {
         if (a.dYx)  // folded BN backward: 1x1 convs only (ops/conv.py conv_wgrad_bnfold)
             return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, true>(a, splits, st) : -110;
+        if (a.xbn)  // BN apply + ReLU of X on the staging path: 1x1 convs only
+            return (br32 && a.KH * a.KW == 1) ? launch1<BCO, BKC, WCO, STEM, 4, 32, false, true>(a, splits, st)
+                                               : -111;
     }
     return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32>(a, splits, st)
                 : launch1<BCO, BKC, WCO, STEM, 4, 64>(a, splits, st);
@@ -325,7 +353,8 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     const WgradArgs& a = *args;
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if ((a.stem & 1) && a.dYx) return -110;
+    if ((a.stem & 1) && (a.dYx || a.xbn)) return -110;
+    if (a.dYx && a.xbn) return -111;
     if (a.stem & 1) {
         if (a.Ci != 4 || a.KW > 8 || a.Co % 8) return -102;
         return launch<64, 128, 1, true>(a, splits, st);

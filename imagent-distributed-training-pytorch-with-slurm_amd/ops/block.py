@@ -31,7 +31,8 @@ import os
 import torch
 
 from . import streams
-from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_bwd_coef
+from . import conv as _conv
+from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_bwd_coef, bn_scale_shift
 from .conv import (BNBwdFuse, bnfold_ok, conv_wgrad, conv_wgrad_bnfold, igemm_dgrad, igemm_dgrad_bnfold,
                    igemm_fwd)
 
@@ -45,6 +46,19 @@ _DEFER_WGRAD = os.environ.get("IMAGENT_DEFER_WGRAD", "1") != "0"
 _DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "1") != "0"
 # IMAGENT_SPARSE_DS=0: memset the stride-2 downsample dgrad's output (A/B switch)
 _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
+# IMAGENT_BN_XFUSE=1: the BatchNorm + ReLU before a bottleneck's last (1x1, K = 64 / 128) conv is not a
+# pass of its own: its statistics are finalized into a per-channel scale / shift and the streaming conv
+# applies them (+ ReLU) on its operand load, the weight gradient on its operand staging
+# (ops/conv.py xbn); the BN output is never written or read (saves one write + one read of a 64 / 128
+# channel activation per block at 56x56 / 28x28)
+_XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "0") == "1"
+
+
+def _xfuse_ok(block, x, q) -> bool:
+    conv = block.convs_bns()[-1][0]
+    return (_XFUSE and q is None and x.is_cuda and len(block.convs_bns()) >= 3 and conv.kh == 1 and conv.kw == 1
+            and conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
+            and conv.out_channels % 128 == 0 and not _conv._BNFOLD and not _conv._NOSTREAM)
 
 
 def _fwd(conv, h, bn):
@@ -83,7 +97,11 @@ class _Folded:
 
 
 def _wgrad(conv, dA, h):
-    if isinstance(dA, _Folded):
+    """``h`` is the conv's input, or (BN input, scale / shift) when the BN + ReLU before it is
+    applied on the operand path (``IMAGENT_BN_XFUSE``)."""
+    if isinstance(h, tuple):
+        conv_wgrad(conv, dA, h[0], xbn=h[1])
+    elif isinstance(dA, _Folded):
         conv_wgrad_bnfold(conv, dA.g, dA.x, dA.coef, h)
     else:
         conv_wgrad(conv, dA, h)
@@ -108,14 +126,24 @@ class BlockFn(torch.autograd.Function):
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 ad = _fwd8(ds[0], x, x8, ds[1])
-        for conv, bn, _ in pairs[:-1]:
+        xfuse = _xfuse_ok(block, x, q)
+        ss = None
+        for i, (conv, bn, _) in enumerate(pairs[:-1]):
             a = _fwd8(conv, h, h8, bn)
+            if xfuse and i == len(pairs) - 2:  # BN + ReLU applied by the last conv's operand load
+                ss = bn_scale_shift(a, bn)
+                h = a
+                saved += [a, None]
+                continue
             q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
             h = bn_act_forward(a, None, bn, None, 0, True, q8=q8)
             h8 = (q8[0], q8[1]) if q8 is not None else None
             saved += [a, h]
         conv, bn, _ = pairs[-1]
-        a = _fwd8(conv, h, h8, bn)
+        if ss is not None:
+            a = igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
+        else:
+            a = _fwd8(conv, h, h8, bn)
         q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
         if ds is not None:
             if side is not None:
@@ -140,6 +168,7 @@ class BlockFn(torch.autograd.Function):
         block._last_bn = (a, ad, out) if getattr(block, "_fuse_bnb", False) else None
         block._bnb_done = False
         ctx.block = block
+        ctx.xbn = ss
         ctx.save_for_backward(*saved)
         return out
 
@@ -197,6 +226,7 @@ class BlockFn(torch.autograd.Function):
         block._last_bn = None
         block._bnb_done = False
         fold_done = None  # side-stream event after a folded wgrad that reads dout (= dX, accumulated below)
+        xbn = ctx.xbn  # the last conv's input is BN(acts[-1]) + ReLU applied on its operand load
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             h_in = inputs[i]
@@ -206,8 +236,10 @@ class BlockFn(torch.autograd.Function):
                 if isinstance(dA, _Folded):
                     dH = igemm_dgrad_bnfold(dA.g, dA.x, dA.coef, conv, fz)
                 else:
-                    dH = igemm_dgrad(dA, conv.wt_bf16, (h_in.shape[1], h_in.shape[2]), conv.stride,
+                    dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
+                if h_in is None:  # xfuse (i == n - 1): the weight gradient applies the BN on its staging
+                    h_in = (acts[i - 1], xbn)
                 if not _DEFER_WGRAD:
                     _wgrad(conv, dA, h_in)
                 dA_w = dA

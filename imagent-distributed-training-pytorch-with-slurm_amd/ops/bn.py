@@ -35,6 +35,24 @@ def stats_finalize(work, rows: int) -> None:
                "bn stats finalize")
 
 
+def bn_scale_shift(x: torch.Tensor, bn) -> torch.Tensor:
+    """Training-mode BatchNorm whose apply + ReLU runs on the consumer conv's operand load
+    (``igemm_fwd(xbn=)`` / ``conv_wgrad(xbn=)``): finalize the conv epilogue's statistics of ``x``
+    and return ss [2, C] = (gamma * rstd, beta - mean * gamma * rstd); ``bn.work.save`` gets
+    (mean, rstd) for the backward and ``bn.work.stats`` (mean, var) for the running statistics,
+    exactly as :func:`bn_act_forward` leaves them. One launch; the BN output is never written."""
+    from .conv import _SHIFT
+    w = bn.work
+    S, _, C = w.slab.shape
+    R = x.numel() // C
+    ss = torch.empty((2, C), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.kernels().imk_bn_finalize_affine(w.slab.data_ptr(), w.save.data_ptr(), w.stats.data_ptr(),
+                                                     bn.weight.data_ptr(), bn.bias.data_ptr(), ss.data_ptr(), S, C,
+                                                     R, bn.eps, 1 if _SHIFT else 0, _lib.stream_ptr()),
+               "bn finalize + affine")
+    return ss
+
+
 def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
                   save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False, q8=None):
     """``q8 = (y8 uint8, exp int32[1], amax f32[1])``: also write the e4m3 copy of y."""

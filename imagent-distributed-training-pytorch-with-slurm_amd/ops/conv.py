@@ -73,7 +73,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
               tile: int = 0, stem: bool = False, epi: int = 0,
               fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, affine: Optional[torch.Tensor] = None,
-              accumulate: bool = False) -> torch.Tensor:
+              accumulate: bool = False, xbn: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` (a [STAT_SLOTS, 2, Co]
     slab), or, given a BatchNorm workspace (``bn.work``), into its slab as
@@ -86,7 +86,10 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     w*2^-ew, ex/ew device int32 scalars; the block-scaled MFMA restores the
     scales (Ci % 16 == 0).
     ``affine`` [2, Co] fp32 (scale, shift): an inference BatchNorm folded into
-    the epilogue (before ``accumulate`` into ``out`` and ``relu``)."""
+    the epilogue (before ``accumulate`` into ``out`` and ``relu``).
+    ``xbn`` [2, Ci] fp32 (scale, shift): the operand is relu(x * scale + shift) -- the producing
+    BatchNorm's apply + ReLU done on this conv's operand load (1x1, Ci in {64, 128}: the
+    streaming kernel; see :func:`ops.bn.bn_scale_shift`)."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
@@ -112,6 +115,9 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
         a.xexp, a.wexp = fp8[0].data_ptr(), fp8[1].data_ptr()
     if bias is not None:
         a.bias = bias.data_ptr()
+    if xbn is not None:
+        assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
+        a.xbn = xbn.data_ptr()
     if stats is not None:
         if hasattr(stats, "slab"):  # a BatchNorm's workspace: shifted sums around its last batch mean
             if _SHIFT:
@@ -223,9 +229,10 @@ class BNBwdFuse:
 
 
 def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int, KH: int,
-                KW: int, splits: int = 0, stem: bool = False) -> None:
+                KW: int, splits: int = 0, stem: bool = False, xbn: Optional[torch.Tensor] = None) -> None:
     """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci]).
-    ``stem``: x has 4 channels, dw is ``[Co][KH][32]`` (see :func:`igemm_fwd`)."""
+    ``stem``: x has 4 channels, dw is ``[Co][KH][32]`` (see :func:`igemm_fwd`).
+    ``xbn``: the X operand is relu(x * xbn[0] + xbn[1]) (1x1 convs; as in :func:`igemm_fwd`)."""
     N, H, W, Ci = x.shape
     _, OH, OW, Co = dy.shape
     if stem:
@@ -239,6 +246,9 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     a.m_per_split = 0
     a.mg_ohw, a.sh_ohw = _magic(OH * OW)
     a.mg_ow, a.sh_ow = _magic(OW)
+    if xbn is not None:
+        assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
+        a.xbn = xbn.data_ptr()
     _lib.check(_lib.kernels().imk_conv_wgrad(C.byref(a), splits, _lib.stream_ptr()), "conv wgrad")
 
 
@@ -345,22 +355,26 @@ class ConvFn(torch.autograd.Function):
         return dx, None, None, None
 
 
-def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
+def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tensor] = None) -> None:
     """Accumulate a Conv2d module's weight gradient into its arena slot and
     signal the bucketed reducer (on the wgrad side stream when enabled,
-    ``ops/streams.py``)."""
+    ``ops/streams.py``). ``xbn``: x is a BatchNorm's INPUT whose apply + ReLU
+    the kernel does on its operand staging (:func:`igemm_wgrad`)."""
     side = streams.side_stream(dy.device) if dy.is_cuda else None
     if side is None:
-        _conv_wgrad(mod, dy, x)
+        _conv_wgrad(mod, dy, x, xbn)
         return
     side.wait_stream(torch.cuda.current_stream(dy.device))
     with torch.cuda.stream(side):
-        _conv_wgrad(mod, dy, x)
-    streams.protect(dy, x)
+        _conv_wgrad(mod, dy, x, xbn)
+    if xbn is not None:
+        streams.protect(dy, x, xbn)
+    else:
+        streams.protect(dy, x)
     streams.ensure_join_after_backward()
 
 
-def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
+def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tensor] = None) -> None:
     gp = getattr(mod, "grad_pad", None)
     if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
         gp.zero_()
@@ -368,7 +382,7 @@ def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor) -> None:
         real = gp[:, :, : mod.kw * 4].view(gp.shape[0], mod.kh, mod.kw, 4)[..., : mod.in_channels]
         mod.weight.grad.permute(0, 2, 3, 1).add_(real)
     else:
-        igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw)
+        igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw, xbn=xbn)
     notify_ready(mod.weight)
 
 

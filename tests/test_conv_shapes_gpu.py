@@ -44,23 +44,23 @@ SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _sh
 BENCH_KERNELS = [
     "halo3x3_kernel<56, 4, 0>",
     "halo3x3_kernel<56, 4, 1>",
-    "conv_stream_kernel<128, 128, 2, 0, false>",
-    "conv_stream_kernel<224, 64, 2, 0, true>",
-    "conv_stream_kernel<256, 64, 2, 0, false>",
-    "conv_stream_kernel<256, 64, 2, 2, false>",
-    "conv_stream_kernel<512, 64, 1, 0, false>",
-    "conv_stream_kernel<64, 128, 3, 1, false>",
-    "conv_stream_kernel<64, 256, 3, 0, false>",
-    "conv_stream_kernel<64, 64, 3, 0, false>",
+    "conv_stream_kernel<128, 128, 2, 0, false, false>",
+    "conv_stream_kernel<224, 64, 2, 0, true, false>",
+    "conv_stream_kernel<256, 64, 2, 0, false, false>",
+    "conv_stream_kernel<256, 64, 2, 2, false, false>",
+    "conv_stream_kernel<512, 64, 1, 0, false, false>",
+    "conv_stream_kernel<64, 128, 3, 1, false, false>",
+    "conv_stream_kernel<64, 256, 3, 0, false, false>",
+    "conv_stream_kernel<64, 64, 3, 0, false, false>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 2, 2, 0, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 1>",
     "igemm_dma_kernel<256, 256, 2, 2, 0, 8, 2, 2, 0, 1>",
     "igemm_rs_kernel<128, 128, 2, 0, 2>",
-    "wgrad_kernel<128, 128, 2, false, 4, 32, false>",
-    "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
-    "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
-    "wgrad_kernel<64, 128, 1, true, 4, 32, false>",
+    "wgrad_kernel<128, 128, 2, false, 4, 32, false, false>",
+    "wgrad_kernel<128, 128, 2, false, 4, 64, false, false>",
+    "wgrad_kernel<64, 128, 1, false, 4, 32, false, false>",
+    "wgrad_kernel<64, 128, 1, true, 4, 32, false, false>",
 ]
 
 

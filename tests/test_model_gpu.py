@@ -87,6 +87,19 @@ def test_hip_vs_torch_forward_backward(arch, fused):
         assert rel(model(x), ref(xr)) < max(5e-2, 2.0 * ebf)
 
 
+def test_bn_operand_fusion_matches_torch(monkeypatch):
+    """IMAGENT_BN_XFUSE: every bottleneck's bn2 + ReLU applied on conv3's operand load (forward)
+    and weight-gradient staging; logits, every parameter gradient and the BN buffers against the
+    fp32 PyTorch model, as the unfused path is checked (test_hip_vs_torch_forward_backward)."""
+    from imagent_amd.ops import block
+    monkeypatch.setattr(block, "_XFUSE", True)
+    calls = []
+    real = block.bn_scale_shift
+    monkeypatch.setattr(block, "bn_scale_shift", lambda a, bn: calls.append(1) or real(a, bn))
+    test_hip_vs_torch_forward_backward("resnet50", True)
+    assert len(calls) == 7, len(calls)  # the 3 + 4 bottlenecks of stages 1-2 (conv3 K = 64 / 128)
+
+
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_fused_bn_backward_matches_unfused(arch):
     """IG_BNBWD (BN-backward reductions in the dgrad epilogue, cross-block
