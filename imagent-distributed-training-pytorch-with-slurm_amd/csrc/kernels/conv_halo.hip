@@ -85,7 +85,20 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         *reinterpret_cast<u32x4*>(sW + (t * 64 + n) * 128 + ((c ^ (n & 7)) << 4)) = v;
     }
 
+    // a.xbn (forward): the patch is relu(x * scale + shift) per channel -- the producing BatchNorm's
+    // apply + ReLU done while staging (ops/block.py); out-of-image pixels stay 0. A thread's chunks all
+    // hold channels (tid & 7) * 8 .. + 7, so its 16 constants live in registers
+    const bool xbn = EPI == 0 && a.xbn != nullptr;
+    float xsc[8], xsh[8];
+    if (xbn) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            xsc[k] = a.xbn[(tid & 7) * 8 + k];
+            xsh[k] = a.xbn[64 + (tid & 7) * 8 + k];
+        }
+    }
     u32x4 pr[PMAX];
+    bool pv[PMAX];  // chunk inside the image (xbn: transformed at staging)
     auto load_patch = [&](int band) {
         const int img = band / bands_per_img, y0 = (band - img * bands_per_img) * R;
         const bf16_t* xi = a.X + (size_t)img * a.H * W * 64;
@@ -93,12 +106,15 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         for (int i = 0; i < PMAX; ++i) {
             const int id = tid + i * 512;
             u32x4 v = {0u, 0u, 0u, 0u};
+            pv[i] = false;
             if (id < NCH) {
                 const int c = id & 7, pix = id >> 3;
                 const int prow = pix / PCOLS, pcol = pix - prow * PCOLS;
                 const int iy = y0 - 1 + prow, ix = pcol - 1;
-                if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)W)
+                if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)W) {
                     v = *reinterpret_cast<const u32x4*>(xi + ((size_t)iy * W + ix) * 64 + c * 8);
+                    pv[i] = true;
+                }
             }
             pr[i] = v;
         }
@@ -111,7 +127,14 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                 const int c = id & 7, pix = id >> 3;
                 const int prow = pix / PCOLS, pcol = pix - prow * PCOLS;
                 const int q = prow * PW + pcol;
-                *reinterpret_cast<u32x4*>(sP + q * 128 + ((c ^ (q & 7)) << 4)) = pr[i];
+                u32x4 v = pr[i];
+                if (xbn && pv[i]) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        v[k] = pack_bf2(fmaxf(fmaf(lo_bf(v[k]), xsc[2 * k], xsh[2 * k]), 0.f),
+                                        fmaxf(fmaf(hi_bf(v[k]), xsc[2 * k + 1], xsh[2 * k + 1]), 0.f));
+                }
+                *reinterpret_cast<u32x4*>(sP + q * 128 + ((c ^ (q & 7)) << 4)) = v;
             }
         }
     };

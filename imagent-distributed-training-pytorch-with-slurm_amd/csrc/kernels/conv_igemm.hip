@@ -120,7 +120,14 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
         return launch_rs<128, 64, 1, 2>(a, st);
     }
-    if (a.xbn) return (a.flags & (IG_FP8 | IG_OUT_F32 | IG_RELU | IG_AFFINE | IG_STEM)) ? -120 : conv_stream(a, st);
+    if (a.xbn) {  // the operand BN + ReLU: the halo kernel (64 -> 64 3x3) or the streaming 1x1, nothing else
+        if (a.flags & (IG_FP8 | IG_OUT_F32 | IG_RELU | IG_AFFINE | IG_STEM | IG_BNBWD | IG_ACCUM)) return -120;
+        if (a.nth == 3 && a.ntw == 3) {
+            const int r = conv_halo(a, st);
+            return r == 1 ? -120 : r;
+        }
+        return conv_stream(a, st);
+    }
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
     if (a.X2) return conv_stream(a, st);  // folded BN backward: the streaming kernel only
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps

@@ -41,7 +41,7 @@ struct WgradArgs {
     const bf16_t* dYx;
     const float* dYcoef;
     // the X operand is relu(X * xbn[c] + xbn[Ci + c]) (BatchNorm apply + ReLU of the conv's input,
-    // never materialised: ops/block.py); 1x1 convs
+    // never materialised: ops/block.py); out-of-image taps stay 0
     const float* xbn;
 };
 
@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
 // half the operand bytes per MFMA FLOP of a 128x128 tile)
 // BR: pixels (reduction rows) per stage -- 64, or 32 (half the LDS: three
 // 4-wave blocks per CU instead of two, more waves to hide the load latency)
-// XB: the X operand gets the BatchNorm apply + ReLU of a.xbn while it is staged (1x1 convs)
+// XB: the X operand gets the BatchNorm apply + ReLU of a.xbn while it is staged
 template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false, bool XB = false>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgrad_kernel(const WgradArgs a) {
     constexpr int NT = NW * 64;
@@ -339,9 +339,9 @@ int launch(WgradArgs a, int splits, hipStream_t st) {
     if constexpr (!STEM) {
         if (a.dYx)  // folded BN backward: 1x1 convs only (ops/conv.py conv_wgrad_bnfold)
             return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, true>(a, splits, st) : -110;
-        if (a.xbn)  // BN apply + ReLU of X on the staging path: 1x1 convs only
-            return (br32 && a.KH * a.KW == 1) ? launch1<BCO, BKC, WCO, STEM, 4, 32, false, true>(a, splits, st)
-                                               : -111;
+        if (a.xbn)  // BN apply + ReLU of X on the staging path (padding taps stay 0)
+            return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, false, true>(a, splits, st)
+                        : launch1<BCO, BKC, WCO, STEM, 4, 64, false, true>(a, splits, st);
     }
     return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32>(a, splits, st)
                 : launch1<BCO, BKC, WCO, STEM, 4, 64>(a, splits, st);

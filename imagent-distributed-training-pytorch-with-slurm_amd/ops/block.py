@@ -46,19 +46,28 @@ _DEFER_WGRAD = os.environ.get("IMAGENT_DEFER_WGRAD", "1") != "0"
 _DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "1") != "0"
 # IMAGENT_SPARSE_DS=0: memset the stride-2 downsample dgrad's output (A/B switch)
 _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
-# IMAGENT_BN_XFUSE=1: the BatchNorm + ReLU before a bottleneck's last (1x1, K = 64 / 128) conv is not a
-# pass of its own: its statistics are finalized into a per-channel scale / shift and the streaming conv
-# applies them (+ ReLU) on its operand load, the weight gradient on its operand staging
-# (ops/conv.py xbn); the BN output is never written or read (saves one write + one read of a 64 / 128
-# channel activation per block at 56x56 / 28x28)
-_XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "0") == "1"
+# IMAGENT_BN_XFUSE (default 1; 0 = A/B off): a BatchNorm + ReLU inside a block whose consumer conv can
+# take it on its operand path is not a pass of its own: its statistics are finalized into a per-channel
+# scale / shift and the consumer applies them (+ ReLU) on its operand load -- the streaming 1x1 conv
+# (a bottleneck's conv3 with K = 64 / 128) or the halo-tiled 64 -> 64 3x3 conv (the stage-1 conv2 of
+# ResNet-50 at 56x56, of ResNet-18/34 at 56x56 / 112x112) -- and its weight gradient on the operand
+# staging (ops/conv.py xbn); the BN output is never written or read. Measured at R50 / 1024 with the
+# 1x1 consumers: +0.43 % img/s (12,499 / 12,497 vs 12,446 / 12,440, same box)
+_XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "1") != "0"
+_HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
 
 
-def _xfuse_ok(block, x, q) -> bool:
-    conv = block.convs_bns()[-1][0]
-    return (_XFUSE and q is None and x.is_cuda and len(block.convs_bns()) >= 3 and conv.kh == 1 and conv.kw == 1
-            and conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
-            and conv.out_channels % 128 == 0 and not _conv._BNFOLD and not _conv._NOSTREAM)
+def _xfuse_ok(conv, a, q) -> bool:
+    """Can ``conv`` (the consumer of BN(a) + ReLU) apply that BN on its operand path?"""
+    if not (_XFUSE and q is None and a.is_cuda) or _conv._BNFOLD or _conv._NOSTREAM:
+        return False
+    if conv.kh == 1 and conv.kw == 1:
+        return (conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
+                and conv.out_channels % 128 == 0)
+    W = a.shape[2]
+    return (_HALO and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
+            and conv.in_channels == 64 and conv.out_channels == 64 and a.shape[1] == W
+            and ((W == 56 and W % 4 == 0) or (W == 112 and a.shape[1] % 2 == 0)))
 
 
 def _fwd(conv, h, bn):
@@ -126,13 +135,15 @@ class BlockFn(torch.autograd.Function):
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 ad = _fwd8(ds[0], x, x8, ds[1])
-        xfuse = _xfuse_ok(block, x, q)
+        xbn = [None] * len(pairs)  # xbn[i]: conv i applies the preceding BN + ReLU on its operand load
         ss = None
         for i, (conv, bn, _) in enumerate(pairs[:-1]):
-            a = _fwd8(conv, h, h8, bn)
-            if xfuse and i == len(pairs) - 2:  # BN + ReLU applied by the last conv's operand load
-                ss = bn_scale_shift(a, bn)
-                h = a
+            a = _fwd8(conv, h, h8, bn) if ss is None else \
+                igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
+            ss = None
+            if _xfuse_ok(pairs[i + 1][0], a, q):
+                ss = xbn[i + 1] = bn_scale_shift(a, bn)
+                h, h8 = a, None
                 saved += [a, None]
                 continue
             q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
@@ -168,7 +179,7 @@ class BlockFn(torch.autograd.Function):
         block._last_bn = (a, ad, out) if getattr(block, "_fuse_bnb", False) else None
         block._bnb_done = False
         ctx.block = block
-        ctx.xbn = ss
+        ctx.xbn = xbn
         ctx.save_for_backward(*saved)
         return out
 
@@ -226,7 +237,7 @@ class BlockFn(torch.autograd.Function):
         block._last_bn = None
         block._bnb_done = False
         fold_done = None  # side-stream event after a folded wgrad that reads dout (= dX, accumulated below)
-        xbn = ctx.xbn  # the last conv's input is BN(acts[-1]) + ReLU applied on its operand load
+        xbn = ctx.xbn  # xbn[i]: conv i's input is BN(acts[i - 1]) + ReLU applied on its operand path
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             h_in = inputs[i]
@@ -238,8 +249,8 @@ class BlockFn(torch.autograd.Function):
                 else:
                     dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
-                if h_in is None:  # xfuse (i == n - 1): the weight gradient applies the BN on its staging
-                    h_in = (acts[i - 1], xbn)
+                if h_in is None:  # xfuse: the weight gradient applies the BN on its operand staging
+                    h_in = (acts[i - 1], xbn[i])
                 if not _DEFER_WGRAD:
                     _wgrad(conv, dA, h_in)
                 dA_w = dA

@@ -52,6 +52,10 @@ BENCH_KERNELS = [
     "conv_stream_kernel<64, 128, 3, 1, false, false>",
     "conv_stream_kernel<64, 256, 3, 0, false, false>",
     "conv_stream_kernel<64, 64, 3, 0, false, false>",
+    "conv_stream_kernel<64, 256, 3, 0, false, true>",
+    "conv_stream_kernel<128, 128, 2, 0, false, true>",
+    "wgrad_kernel<128, 128, 2, false, 4, 32, false, true>",
+    "wgrad_kernel<64, 128, 1, false, 4, 32, false, true>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 2, 2, 0, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 1>",
@@ -184,6 +188,20 @@ def test_production_conv_shape(shape):
     wref = torch.nn.grad.conv2d_weight(x[..., :Ci].permute(0, 3, 1, 2).float(), (Co, Ci, k, k),
                                        g.permute(0, 3, 1, 2).float(), s, p)
     assert rel(got.permute(0, 3, 1, 2), wref) < 1e-2
+
+    if s == 1 and ((k == 1 and Ci in (64, 128) and Co % 128 == 0) or
+                   (k == 3 and Ci == Co == 64 and H in (56, 112))):
+        # ---- BN apply + ReLU on the operand path (IMAGENT_BN_XFUSE: bottleneck conv3's of stages 1-2, the
+        # halo-tiled 64 -> 64 3x3 convs)
+        ss = torch.stack([torch.rand(Ci, device=DEV) + 0.5, torch.randn(Ci, device=DEV) * 0.3]).contiguous()
+        hx = torch.relu(x.float() * ss[0] + ss[1]).to(torch.bfloat16)
+        yx, rec["fwd_xbn"] = _kernels(lambda: igemm_fwd(x, w, 1, p, k, k, stats=slab, xbn=ss))
+        assert rel(yx[SEL].permute(0, 3, 1, 2), F.conv2d(hx[SEL].permute(0, 3, 1, 2).float(), wr, None, 1, p)) < 1e-2
+        dwx = torch.zeros(Co, k * k * Ci, device=DEV)
+        _, rec["wgrad_xbn"] = _kernels(lambda: igemm_wgrad(g, x, dwx, 1, p, k, k, xbn=ss))
+        wxr = torch.nn.grad.conv2d_weight(hx.permute(0, 3, 1, 2).float(), (Co, Ci, k, k),
+                                          g.permute(0, 3, 1, 2).float(), 1, p)
+        assert rel(dwx.view(Co, k, k, Ci).permute(0, 3, 1, 2), wxr) < 1e-2
 
     for op, names in rec.items():
         assert names, f"{op}: the profiler saw no conv kernel (auto-dispatch launched nothing?)"

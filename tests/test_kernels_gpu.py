@@ -141,31 +141,34 @@ def test_conv_pingpong(tile, shape):
     test_conv_lds_epilogue(tile, shape)
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 14, 256), (3, 64, 9, 128), (2, 128, 11, 512), (5, 128, 7, 128)])
+@pytest.mark.parametrize("shape", [(4, 64, 14, 256, 1), (3, 64, 9, 128, 1), (2, 128, 11, 512, 1), (5, 128, 7, 128, 1),
+                                   (3, 64, 56, 64, 3), (2, 64, 112, 64, 3)])
 def test_conv_xbn_operand(shape):
     """BatchNorm apply + ReLU on the operand path (IMAGENT_BN_XFUSE): the streaming 1x1 forward
     (with statistics) and the weight gradient take the BN INPUT x and a per-channel (scale, shift),
     against fp32 convs of relu(x * scale + shift) rounded to bf16 (what the BN pass would store);
     negative scales, ragged pixel counts."""
     from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
-    N, Ci, H, Co = shape
+    N, Ci, H, Co, k = shape  # k = 3: the halo-tiled 64 -> 64 kernel (zero padding must stay 0)
+    p = k // 2
     torch.manual_seed(11)
     x = bf(torch.randn(N, H, H, Ci, device=DEV) * 2 + 0.5)
     ss = torch.stack([torch.randn(Ci, device=DEV), torch.randn(Ci, device=DEV) * 0.5]).contiguous()
     h = torch.relu(x.float() * ss[0] + ss[1]).to(torch.bfloat16).float()  # [N, H, W, Ci]
-    w = bf(torch.randn(Co, 1, 1, Ci, device=DEV) * (2.0 / Ci) ** 0.5)
-    ref = F.conv2d(h.permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2))  # NCHW
+    w = bf(torch.randn(Co, k, k, Ci, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5)
+    wr = w.float().permute(0, 3, 1, 2)
+    ref = F.conv2d(h.permute(0, 3, 1, 2), wr, None, 1, p)  # NCHW
     slab = torch.zeros(32, 2, Co, device=DEV)
-    y = igemm_fwd(x, w, 1, 0, 1, 1, stats=slab, xbn=ss)
+    y = igemm_fwd(x, w, 1, p, k, k, stats=slab, xbn=ss)
     assert rel(y.permute(0, 3, 1, 2), ref) < 1e-2
     yb = y.float()
     assert rel(slab.sum(0)[0], yb.sum((0, 1, 2))) < 1e-3
     assert rel(slab.sum(0)[1], (yb * yb).sum((0, 1, 2))) < 1e-3
     g = bf(torch.randn(N, H, H, Co, device=DEV))
-    dw = torch.zeros(Co, Ci, device=DEV)
-    igemm_wgrad(g, x, dw, 1, 0, 1, 1, xbn=ss)
-    wref = torch.einsum("nhwo,nhwc->oc", g.float(), h)
-    assert rel(dw, wref) < 1e-2
+    dw = torch.zeros(Co, k * k * Ci, device=DEV)
+    igemm_wgrad(g, x, dw, 1, p, k, k, xbn=ss)
+    wref = torch.nn.grad.conv2d_weight(h.permute(0, 3, 1, 2), (Co, Ci, k, k), g.float().permute(0, 3, 1, 2), 1, p)
+    assert rel(dw.view(Co, k, k, Ci).permute(0, 3, 1, 2), wref) < 1e-2
 
 
 @pytest.mark.parametrize("splits", [0, 3])
