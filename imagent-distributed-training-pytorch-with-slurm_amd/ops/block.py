@@ -53,7 +53,9 @@ _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 # ResNet-50 at 56x56, of ResNet-18/34 at 56x56 / 112x112) -- and its weight gradient on the operand
 # staging (ops/conv.py xbn); the BN output is never written or read. Measured at R50 / 1024 with the
 # 1x1 consumers: +0.43 % img/s (12,499 / 12,497 vs 12,446 / 12,440, same box)
+# (IMAGENT_BN_XFUSE=all: also the halo 3x3 consumers -- numerics-tested, not yet measured in the step)
 _XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "1") != "0"
+_XFUSE_3X3 = os.environ.get("IMAGENT_BN_XFUSE", "1") == "all"
 _HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
 
 
@@ -65,7 +67,7 @@ def _xfuse_ok(conv, a, q) -> bool:
         return (conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
                 and conv.out_channels % 128 == 0)
     W = a.shape[2]
-    return (_HALO and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
+    return (_HALO and _XFUSE_3X3 and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
             and conv.in_channels == 64 and conv.out_channels == 64 and a.shape[1] == W
             and ((W == 56 and W % 4 == 0) or (W == 112 and a.shape[1] % 2 == 0)))
 

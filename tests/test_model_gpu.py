@@ -114,6 +114,7 @@ def test_bn_operand_fusion_halo_matches_unfused(monkeypatch):
     img = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device=DEV)
     lab = torch.randint(0, 1000, (8,), device=DEV)
     grads, bufs = [], []
+    monkeypatch.setattr(block, "_XFUSE_3X3", True)
     for on in (False, True):
         monkeypatch.setattr(block, "_XFUSE", on)
         calls = []
