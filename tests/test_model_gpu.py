@@ -30,7 +30,7 @@ def _grads(model, x, lab, autocast=False):
 
 
 @pytest.mark.parametrize("arch,fused", [("resnet18", True), ("resnet50", True), ("resnet50", False)])
-def test_hip_vs_torch_forward_backward(arch, fused):
+def test_hip_vs_torch_forward_backward(arch, fused, H=64):
     from imagent_amd.models import resnet
     from imagent_amd.models.native import bind_native
     from imagent_amd.ops.misc import normalize_u8
@@ -43,7 +43,7 @@ def test_hip_vs_torch_forward_backward(arch, fused):
         for p_ref, p in zip(ref.parameters(), model.parameters()):
             p_ref.copy_(p.to(torch.bfloat16).float())
     ref_bf = copy.deepcopy(ref)
-    B, H = 16, 64
+    B = 16
     low = torch.rand(B, 3, 8, 8, device=DEV)
     img = (F.interpolate(low, size=(H, H), mode="bicubic", align_corners=False).clamp(0, 1) * 255)
     img = img.to(torch.uint8).permute(0, 2, 3, 1).contiguous()
@@ -100,48 +100,18 @@ def test_bn_operand_fusion_matches_torch(monkeypatch):
     assert len(calls) == 7, len(calls)  # conv3 K = 64 / 128 of stages 1-2 (the 64x64 test input has no 56x56 halo conv)
 
 
-def test_bn_operand_fusion_halo_matches_unfused(monkeypatch):
-    """IMAGENT_BN_XFUSE with the halo consumer: ResNet-18 at 224 (stage-1 conv2 64 -> 64 3x3 at 56x56
-    takes bn1 + ReLU on its patch staging); every gradient of one training step and the updated BN
-    buffers match the unfused HIP path (same bf16 kernels otherwise) within atomic-order noise."""
-    import copy
-    from imagent_amd.models import resnet
-    from imagent_amd.models.native import bind_native
+def test_bn_operand_fusion_halo_matches_torch(monkeypatch):
+    """IMAGENT_BN_XFUSE=all with the halo consumer: ResNet-18 at 224 (the stage-1 conv2, 64 -> 64 3x3 at
+    56x56, takes bn1 + ReLU on its patch staging, its weight gradient on the operand staging): logits,
+    every parameter gradient and the BN buffers against the fp32 PyTorch model."""
     from imagent_amd.ops import block
-    from imagent_amd.ops.misc import normalize_u8
-    torch.manual_seed(0)
-    base = resnet.build("resnet18", num_classes=1000).to(DEV)
-    img = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device=DEV)
-    lab = torch.randint(0, 1000, (8,), device=DEV)
-    grads, bufs = [], []
+    monkeypatch.setattr(block, "_XFUSE", True)
     monkeypatch.setattr(block, "_XFUSE_3X3", True)
-    for on in (False, True):
-        monkeypatch.setattr(block, "_XFUSE", on)
-        calls = []
-        real = block.bn_scale_shift
-        monkeypatch.setattr(block, "bn_scale_shift", lambda a, bn: calls.append(1) or real(a, bn))
-        m = copy.deepcopy(base)
-        st = bind_native(m, DEV)
-        m.train()
-        st.arena.zero_grad()
-        x = normalize_u8(img, (224, 224), 4, (0.5,) * 3, (0.5,) * 3)
-        F.cross_entropy(m(x), lab).backward()
-        torch.cuda.synchronize()
-        grads.append({n: p.grad.float().clone() for n, p in m.named_parameters()})
-        bufs.append({n: b.float().clone() for n, b in m.named_buffers()})
-        assert len(calls) == (2 if on else 0), calls  # the two stage-1 BasicBlocks
-        monkeypatch.setattr(block, "bn_scale_shift", real)
-    # two backward passes differ by atomic-order BN statistics (ReLU-mask flips near 0 on a random-init
-    # net: see test_graphed_step_matches_eager), so per parameter the projection ratio, overall the norm
-    for n in grads[0]:
-        g0, g1 = grads[0][n], grads[1][n]
-        ratio = ((g1 * g0).sum() / (g0 * g0).sum().clamp_min(1e-30)).item()
-        assert abs(ratio - 1.0) < 0.1, (n, ratio)
-    cat = lambda d: torch.cat([v.flatten() for v in d.values()])  # noqa: E731
-    assert rel(cat(grads[1]), cat(grads[0])) < 3e-2
-    for n in bufs[0]:
-        if "num_batches_tracked" not in n:
-            assert rel(bufs[1][n], bufs[0][n]) < 1e-2, n
+    calls = []
+    real = block.bn_scale_shift
+    monkeypatch.setattr(block, "bn_scale_shift", lambda a, bn: calls.append(1) or real(a, bn))
+    test_hip_vs_torch_forward_backward("resnet18", True, H=224)
+    assert len(calls) == 2, len(calls)  # the two stage-1 BasicBlocks
 
 
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
