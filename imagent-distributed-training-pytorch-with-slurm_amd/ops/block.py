@@ -53,7 +53,8 @@ _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 # ResNet-50 at 56x56, of ResNet-18/34 at 56x56 / 112x112) -- and its weight gradient on the operand
 # staging (ops/conv.py xbn); the BN output is never written or read. Measured at R50 / 1024 with the
 # 1x1 consumers: +0.43 % img/s (12,499 / 12,497 vs 12,446 / 12,440, same box)
-# (IMAGENT_BN_XFUSE=all: also the halo 3x3 consumers -- numerics-tested, not yet measured in the step)
+# (IMAGENT_BN_XFUSE=all: also the halo 3x3 consumers -- numerics-tested, measured -0.3 % at R50 / 1024 and
+# R18 448^2: the patch staging's extra VALU costs more than the skipped pass saves; opt-in)
 _XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "1") != "0"
 _XFUSE_3X3 = os.environ.get("IMAGENT_BN_XFUSE", "1") == "all"
 _HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
