@@ -91,6 +91,9 @@ def main(argv=None):
                     help="1: capture the whole step in a HIP graph and replay it (1 GPU; launch-bound small batches)")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
                     help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
+    ap.add_argument("--eval", type=int, default=0,
+                    help="N > 0: after the timed training steps, also time N validation steps (the folded-BN eval "
+                         "forward + loss + top-k counters, imagenet.py:166-210) and report val_img_s")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
                     help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward; fp32: the reference's own "
                          "precision (imagenet.py:312 trains fp32), PyTorch/MIOpen path only (--kernels torch)")
@@ -106,7 +109,7 @@ def main(argv=None):
     from imagent_amd.models import resnet
     from imagent_amd.models.arena import ParamArena
     from imagent_amd.parallel import launcher
-    from imagent_amd.parallel.comm import make_communicator
+    from imagent_amd.parallel.comm import make_communicator, rccl_communicators
     from imagent_amd.parallel.ddp import DataParallel
     from imagent_amd.parallel.dist import init_distributed
     from imagent_amd.train.engine import StepRunner
@@ -144,6 +147,15 @@ def main(argv=None):
                 auto_reduced = True
                 print(f"bench: {free:.1f} GiB of HBM free, running {a.batch_size} img/GPU", file=sys.stderr,
                       flush=True)
+
+    def max_over_ranks(seconds: float) -> float:
+        # the c10d default group is CPU-side gloo for nccl jobs (parallel/dist.py): reduce a host tensor
+        t = torch.tensor([seconds], dtype=torch.float64)
+        if ctx.world_size > 1:
+            if ctx.c10d_backend == "nccl":
+                t = t.to(ctx.device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t.item())
 
     def run():
         dev = ctx.device
@@ -204,11 +216,27 @@ def main(argv=None):
         ctx.barrier()
         t1 = time.perf_counter()
         coll_per_step = (comm.collectives - c0) / max(1, a.steps)
-        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        if ctx.world_size > 1:
-            torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
-        T = float(elapsed.item())
+        T = max_over_ranks(t1 - t0)
         loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
+        n_rccl = rccl_communicators()  # counted while the training communicator is open
+        val = None
+        if a.eval > 0:  # validation throughput (Trainer.validate's step): eval-mode forward under no_grad
+            model.eval()
+            vsrc = src.batches(a.eval + 2)
+            for _ in range(2):
+                u8, y = next(vsrc)
+                runner.eval_step(tf(u8), y)
+            ctx.barrier()
+            sync()
+            v0 = time.perf_counter()
+            for u8, y in vsrc:
+                runner.eval_step(tf(u8), y)
+            sync()
+            ctx.barrier()
+            Tv = max_over_ranks(time.perf_counter() - v0)
+            val = dict(val_img_s=round(a.gpus * a.batch_size * a.eval / Tv, 2), val_steps=a.eval,
+                       val_ms_per_step=round(1000.0 * Tv / a.eval, 3))
+            model.train()
         value = a.gpus * a.batch_size * a.steps / T
         base = BASELINES.get((a.arch, a.image_size))
         if ctx.rank == 0:
@@ -242,6 +270,8 @@ def main(argv=None):
                                        f"{coll_per_step:g} collectives/step" if coll_per_step > 0 else
                                        "none (world of one, collectives skipped)"),
                     "comm": comm.name,
+                    "rccl_communicators_per_process": n_rccl,
+                    "c10d_backend": ctx.c10d_backend,
                     "world_size": ctx.world_size,
                     "comm_nranks": getattr(comm, "nranks", comm.world_size),
                     "collectives_per_step": coll_per_step,
@@ -256,6 +286,8 @@ def main(argv=None):
                     if dev.type == "cuda" else None,
                 },
             }
+            if val:
+                out.update(val)
             print(json.dumps(out), flush=True)
         comm.close()
 

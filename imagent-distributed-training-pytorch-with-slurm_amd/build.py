@@ -9,8 +9,10 @@
   tracker, ``csrc/runtime``), plain C++.
 
 All three expose a C ABI and are loaded with ctypes (``ops/_lib.py``), so they
-do not depend on the torch C++ ABI and compile in seconds. The libraries are
-rebuilt only when a source is newer than the output.
+do not depend on the torch C++ ABI. A library is rebuilt when the SHA-256 of its
+sources, headers and compile command differs from the stamp written next to it
+(``<lib>.stamp``) -- content, not mtimes, so a stale ``.so`` that travelled with
+a snapshot (newer mtime than an edited source) is never reused.
 
 Usage: ``python -m imagent_amd.build [--force] [-j N]``
 """
@@ -47,11 +49,28 @@ def _hipcc() -> str:
     return p
 
 
-def _newer(srcs: List[str], out: str) -> bool:
-    if not os.path.exists(out):
+def _digest(srcs: List[str], cmd: List[str]) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    h.update("\0".join(cmd).encode())
+    for s in sorted(srcs):
+        h.update(os.path.basename(s).encode() + b"\0")
+        with open(s, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(srcs: List[str], out: str, cmd: List[str]) -> bool:
+    """True when ``out`` is missing or was built from other sources / flags."""
+    if not os.path.exists(out) or not os.path.exists(out + ".stamp"):
         return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(s) > t for s in srcs)
+    with open(out + ".stamp") as f:
+        return f.read().strip() != _digest(srcs, cmd)
+
+
+def _stamp(srcs: List[str], out: str, cmd: List[str]) -> None:
+    with open(out + ".stamp", "w") as f:
+        f.write(_digest(srcs, cmd) + "\n")
 
 
 def _run(cmd: List[str]) -> None:
@@ -60,9 +79,11 @@ def _run(cmd: List[str]) -> None:
         raise RuntimeError("build failed:\n  " + " ".join(cmd) + "\n" + r.stdout)
 
 
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-Wno-unused-result"]
+
+
 def _compile_hip_object(src: str, obj: str, extra: List[str]) -> str:
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-           "-munsafe-fp-atomics", "-Wno-unused-result"] + extra
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-c", src, "-o", obj] + HIP_FLAGS + extra
     _run(cmd)
     return obj
 
@@ -71,7 +92,8 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
     out = os.path.join(OUT, "libimagent_kernels.so")
-    if not force and not _newer(srcs + hdrs, out):
+    key = ["kernels", ARCH] + HIP_FLAGS
+    if not force and not _stale(srcs + hdrs, out, key):
         return out
     objdir = os.path.join(OUT, "obj")
     os.makedirs(objdir, exist_ok=True)
@@ -81,13 +103,15 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     tl = _torch_lib_dir()
     _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs +
          [f"-L{tl}", f"-Wl,-rpath,{tl}"])
+    _stamp(srcs + hdrs, out, key)
     return out
 
 
 def build_comm(force: bool = False) -> str:
     src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
     out = os.path.join(OUT, "libimagent_comm.so")
-    if not force and not _newer([src], out):
+    key = ["comm", ARCH]
+    if not force and not _stale([src], out, key):
         return out
     os.makedirs(OUT, exist_ok=True)
     tl = _torch_lib_dir()
@@ -96,17 +120,20 @@ def build_comm(force: bool = False) -> str:
         rccl = os.path.join(_rocm(), "lib", "librccl.so")
     _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-x", "hip", f"--offload-arch={ARCH}",
           f"-I{_rocm()}/include", src, "-x", "none", "-o", out, rccl, f"-Wl,-rpath,{tl}"])
+    _stamp([src], out, key)
     return out
 
 
 def build_runtime(force: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     out = os.path.join(OUT, "libimagent_runtime.so")
-    if not force and not _newer(srcs, out):
+    key = ["runtime"]
+    if not force and not _stale(srcs, out, key):
         return out
     os.makedirs(OUT, exist_ok=True)
     cxx = shutil.which("g++") or "c++"
     _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", out] + srcs)
+    _stamp(srcs, out, key)
     return out
 
 

@@ -1,4 +1,4 @@
-// Native RCCL communicator with a dedicated high-priority HIP comm stream.
+// Native RCCL communicator with its own (normal-priority) HIP comm stream.
 //
 // Replaces what the reference gets from c10d ProcessGroupNCCL + NCCL
 // (/root/reference/imagenet.py:270-273 init, :85 metric all-reduce, and the
@@ -23,9 +23,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -52,6 +55,10 @@ thread_local char g_err[512] = {0};
 
 struct Comm {
     ncclComm_t comm = nullptr;
+    // set by imc_abort (the watchdog thread) BEFORE the communicator is torn down: enqueue
+    // paths spinning in settle() on the main thread see it and bail out instead of touching
+    // a communicator that ncclCommAbort is freeing
+    std::atomic<bool> aborting{false};
     hipStream_t stream = nullptr;
     int rank = 0, nranks = 1, device = 0, n_events = 64, stream_mode = 0;
     std::vector<hipEvent_t> events;   // ring of reusable events
@@ -108,20 +115,33 @@ int32_t imc_version() {
 }
 
 // Wait out ncclInProgress on a non-blocking communicator (enqueue calls return
-// it while lazy connection set-up finishes in RCCL's own thread).
-static ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
+// it while lazy connection set-up finishes in RCCL's own thread). Bounded: an
+// abort from the watchdog thread, or SETTLE_LIMIT_S without progress, ends the
+// wait with an error instead of spinning on a communicator being torn down.
+constexpr double SETTLE_LIMIT_S = 600.0;
+
+static ncclResult_t settle(Comm* c, ncclResult_t r) {
+    const auto t0 = std::chrono::steady_clock::now();
     while (r == ncclInProgress) {
+        if (c->aborting.load(std::memory_order_acquire)) return ncclInvalidUsage;
         ncclResult_t st = ncclSuccess;
-        ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+        ncclResult_t q = ncclCommGetAsyncError(c->comm, &st);
         if (q != ncclSuccess) return q;
         r = st;
+        if (r == ncclInProgress &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > SETTLE_LIMIT_S)
+            return ncclSystemError;
     }
     return r;
 }
 
 #define NCCLCALL(c, x)                                                                \
     do {                                                                              \
-        ncclResult_t r_ = settle((c)->comm, (x));                                     \
+        if ((c)->aborting.load(std::memory_order_acquire)) {                          \
+            snprintf(g_err, sizeof(g_err), "communicator aborted");                   \
+            return -3;                                                                \
+        }                                                                             \
+        ncclResult_t r_ = settle((c), (x));                                           \
         if (r_ != ncclSuccess) {                                                      \
             snprintf(g_err, sizeof(g_err), "%s: %s", #x, ncclGetErrorString(r_));     \
             return -2;                                                                \
@@ -253,7 +273,7 @@ int32_t imc_comm_destroy(void* h) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) {
         // a non-blocking communicator finalises asynchronously
-        if (settle(c->comm, ncclCommFinalize(c->comm)) == ncclSuccess) ncclCommDestroy(c->comm);
+        if (settle(c, ncclCommFinalize(c->comm)) == ncclSuccess) ncclCommDestroy(c->comm);
         else ncclCommAbort(c->comm);
     }
     for (auto& e : c->events) (void)hipEventDestroy(e);
@@ -359,11 +379,16 @@ int32_t imc_async_error(void* h) {
     return st == ncclInProgress ? 0 : (int32_t)st;
 }
 
+// Failure path (the watchdog thread): flag first, give an enqueue spinning in settle() on
+// another thread a moment to observe the flag and leave, then abort (unblocks kernels waiting
+// on dead peers). The Comm object itself is never freed here.
 int32_t imc_abort(void* h) {
     Comm* c = static_cast<Comm*>(h);
-    if (c && c->comm) {
-        ncclCommAbort(c->comm);
+    if (c && !c->aborting.exchange(true, std::memory_order_acq_rel) && c->comm) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        ncclComm_t comm = c->comm;
         c->comm = nullptr;
+        ncclCommAbort(comm);
     }
     return 0;
 }

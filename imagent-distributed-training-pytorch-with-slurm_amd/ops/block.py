@@ -67,10 +67,12 @@ def _xfuse_ok(conv, a, q) -> bool:
     if conv.kh == 1 and conv.kw == 1:
         return (conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
                 and conv.out_channels % 128 == 0)
-    W = a.shape[2]
+    H, W = a.shape[1], a.shape[2]
+    # the halo kernel's launch conditions (conv_halo.hip, conv_halo()): W 56 with H % 4 == 0, or W 112 with
+    # H % 2 == 0
     return (_HALO and _XFUSE_3X3 and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
-            and conv.in_channels == 64 and conv.out_channels == 64 and a.shape[1] == W
-            and ((W == 56 and W % 4 == 0) or (W == 112 and a.shape[1] % 2 == 0)))
+            and conv.in_channels == 64 and conv.out_channels == 64
+            and ((W == 56 and H % 4 == 0) or (W == 112 and H % 2 == 0)))
 
 
 def _fwd(conv, h, bn):

@@ -163,6 +163,7 @@ class RcclCommunicator(Communicator):
 
     name = "rccl"
     _instances = 0  # per-process creation counter: every rank creates communicators in the same order
+    live = 0        # communicators currently open in this process
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None,
                  key: Optional[str] = None, self_collectives: Optional[bool] = None,
@@ -244,6 +245,7 @@ class RcclCommunicator(Communicator):
                     fail(f"RCCL ranks did not all come up within {init_timeout:.0f} s")
                 time.sleep(0.001)
         self.stream = torch.cuda.ExternalStream(self.L.imc_comm_stream(h), device=self.device)
+        RcclCommunicator.live += 1
 
     def _chk(self, rc, what):
         if rc != 0:
@@ -316,6 +318,8 @@ class RcclCommunicator(Communicator):
         if getattr(self, "h", None):
             self.L.imc_comm_destroy(self.h)  # synchronises the comm stream first
             self.h = None
+            if hasattr(self, "stream"):
+                RcclCommunicator.live -= 1
         self._held.clear()
 
 
@@ -325,6 +329,28 @@ def _default_store():
         return _get_default_store()
     except Exception:
         return None
+
+
+def _fallback_group(ctx):
+    """The group the c10d fallback reduces over. GPU jobs bootstrap c10d over gloo
+    (:mod:`.dist`), so their fallback creates a ``ProcessGroupNCCL`` HERE, lazily, on
+    every rank together (all ranks reach the fallback together); CPU jobs use the
+    default group."""
+    if getattr(ctx, "device", torch.device("cpu")).type == "cuda" and dist.get_backend() != "nccl":
+        return dist.new_group(backend="nccl")
+    return None
+
+
+def rccl_communicators() -> int:
+    """RCCL communicators this process holds: the own ones plus c10d's NCCL groups."""
+    n = RcclCommunicator.live
+    if dist.is_initialized():
+        try:
+            from torch.distributed.distributed_c10d import _world
+            n += sum(1 for pg in _world.pg_map if dist.get_backend(pg) == "nccl")
+        except Exception:  # private c10d layout moved: count ours only
+            pass
+    return n
 
 
 def make_communicator(ctx, kind: str = "auto") -> Communicator:
@@ -351,7 +377,7 @@ def make_communicator(ctx, kind: str = "auto") -> Communicator:
             # the bootstrap's failure flag makes every rank fail together (RcclCommunicator),
             # so all of them fall back to the c10d group together
             warnings.warn(f"own RCCL communicator unavailable ({e}); using the c10d process group")
-            return TorchCommunicator()
+            return TorchCommunicator(_fallback_group(ctx))
     if kind == "torch":
         if not dist.is_initialized():  # single process without a c10d group: nothing to reduce over
             return LocalCommunicator()

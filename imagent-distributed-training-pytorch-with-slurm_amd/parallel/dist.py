@@ -4,10 +4,17 @@ Reference: ``imagenet.py:267`` binds the device, ``imagenet.py:269-274`` calls
 ``init_process_group(init_method='env://', backend=backend)`` and prints the
 backend; the reference never destroys the group. Here:
 
-* ``backend='nccl'`` is RCCL on ROCm (c10d ``ProcessGroupNCCL``); the gradient
-  all-reduce itself goes through our own RCCL communicator
-  (:mod:`.comm`), the c10d group is kept for rendezvous, barriers and
-  object broadcasts.
+* ``backend='nccl'`` means the collectives run on RCCL (ROCm's NCCL). They go
+  through our OWN RCCL communicator (:mod:`.comm`), so the c10d default group
+  is only bootstrap plumbing (TCPStore rendezvous, barriers, the bench's
+  elapsed-time max): it is created with the CPU-side ``gloo`` backend, and a
+  c10d ``ProcessGroupNCCL`` is created lazily, only on the fallback path where
+  the own communicator cannot start (:func:`.comm.make_communicator`). Every
+  rank then holds exactly ONE RCCL communicator and no c10d NCCL streams: the
+  same stream / hardware-queue layout as the single-GPU bench, which the
+  stream-order study (``profiles/r50_b1024_comm_stream_study.md``) showed is
+  worth 12-26 % img/s. ``IMAGENT_C10D_BACKEND=nccl`` restores an eager c10d
+  NCCL default group (A/B).
 * ``backend='gloo'`` runs the whole framework on CPU (tests, plumbing).
 * a configurable timeout and a clean ``shutdown()``.
 """
@@ -27,9 +34,11 @@ from .launcher import Topology
 class DistContext:
     """The live distributed state of this process."""
 
-    def __init__(self, topo: Topology, backend: str, device: torch.device, initialized: bool):
+    def __init__(self, topo: Topology, backend: str, device: torch.device, initialized: bool,
+                 c10d_backend: Optional[str] = None):
         self.topo = topo
-        self.backend = backend
+        self.backend = backend            # the collective backend the job asked for (--backend)
+        self.c10d_backend = c10d_backend  # the c10d default group's backend (None: no group)
         self.device = device
         self.initialized = initialized
 
@@ -47,7 +56,7 @@ class DistContext:
 
     def barrier(self) -> None:
         if self.initialized and self.world_size > 1:
-            if self.backend == "nccl":
+            if self.c10d_backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
@@ -80,18 +89,31 @@ def init_distributed(topo: Topology, backend: str = "nccl", timeout_s: float = 1
     topo.export_env()
     need_pg = topo.world_size > 1 or os.environ.get("IMAGENT_FORCE_PG") == "1"
     initialized = False
+    c10d = c10d_backend(backend)
     if need_pg and not dist.is_initialized():
         if verbose:
             print("Initializing PyTorch distributed ...")
-        kwargs = dict(init_method="env://", backend=backend,
+        kwargs = dict(init_method="env://", backend=c10d,
                       timeout=datetime.timedelta(seconds=timeout_s),
                       world_size=topo.world_size, rank=topo.global_rank)
-        if backend == "nccl":
+        if c10d == "nccl":
             kwargs["device_id"] = dev
         dist.init_process_group(**kwargs)
         initialized = True
-        if verbose:
-            print(f"Backend: {dist.get_backend()}")
+        if verbose:   # imagenet.py:274 prints the backend
+            print(f"Backend: {backend}" + (f" (collectives on the own RCCL communicator, c10d bootstrap group: "
+                                           f"{dist.get_backend()})" if dist.get_backend() != backend else ""))
     elif dist.is_initialized():
         initialized = True
-    return DistContext(topo, backend, dev, initialized)
+        c10d = dist.get_backend()
+    return DistContext(topo, backend, dev, initialized, c10d if initialized else None)
+
+
+def c10d_backend(backend: str) -> str:
+    """Backend of the c10d default group for a job that asked for ``backend``:
+    ``nccl`` jobs bootstrap over ``gloo`` (their collectives use the own RCCL
+    communicator; module docstring), unless ``IMAGENT_C10D_BACKEND`` says otherwise."""
+    forced = os.environ.get("IMAGENT_C10D_BACKEND")
+    if forced:
+        return forced
+    return "gloo" if backend == "nccl" else backend

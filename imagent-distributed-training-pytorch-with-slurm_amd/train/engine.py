@@ -42,7 +42,7 @@ from ..utils.tb import SummaryWriter
 from .lr import Schedule
 from .meters import AverageMeter, DeviceMetrics
 from .optim import build_optimizer
-from ..utils.watchdog import maybe_stall
+from ..utils.watchdog import maybe_stall, slow_save
 
 
 class StepRunner:
@@ -463,6 +463,12 @@ class Trainer:
             lr = self.last_lr
             va_loss, va1, va5, t_val = self.validate(val_loader)
             total += t_train + t_val
+            # checkpoint I/O is not a hang: every rank disarms its watchdog BEFORE the master starts
+            # writing (the others would otherwise start the next epoch, block in its first collective
+            # and time out while the master writes), and all ranks meet in a barrier after the writes,
+            # still disarmed; the next step's beat re-arms
+            if self.watchdog:
+                self.watchdog.pause()
             if va1 > self.best["top1"]:   # imagenet.py:388-392
                 self.best["top1"], self.best["epoch_top1"] = va1, epoch
                 if self.is_master and a.save_model:
@@ -496,11 +502,12 @@ class Trainer:
             history.append(dict(epoch=epoch + 1, lr=lr, train_loss=tr_loss, val_loss=va_loss, train_top1=tr1,
                                 val_top1=va1, train_top5=tr5, val_top5=va5, train_time=t_train,
                                 val_time=t_val, img_s=ips))
-            if self.watchdog:
-                self.watchdog.pause()  # checkpoint I/O is not a hang
             if a.checkpoint_dir and self.is_master:
+                slow_save()  # fault injection (IMAGENT_FAULT_SLOW_SAVE)
                 ckpt.save_state(os.path.join(a.checkpoint_dir, f"state_{a.arch}.pt"), self.model, self.opt,
                                 epoch, self.best)
+            if self.watchdog and (a.save_model or a.checkpoint_dir):
+                self.ctx.barrier()  # nobody re-arms until the master's writes are done
             if not self.comm.healthy():
                 raise RuntimeError("communicator reported an asynchronous error")
         if self.is_master:   # imagenet.py:422-429

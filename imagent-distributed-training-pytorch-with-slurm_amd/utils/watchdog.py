@@ -13,7 +13,9 @@ thread
    ``torchrun`` / ``srun`` tears down the job instead of it idling for days.
 
 Fault injection for tests: ``IMAGENT_FAULT_STALL=<rank>:<step>:<seconds>``
-makes that rank sleep before that training step (:func:`maybe_stall`).
+makes that rank sleep before that training step (:func:`maybe_stall`);
+``IMAGENT_FAULT_SLOW_SAVE=<seconds>`` makes the master's end-of-epoch checkpoint
+write take that much longer (:func:`slow_save`).
 """
 
 from __future__ import annotations
@@ -90,4 +92,11 @@ def maybe_stall(rank: int, step: int) -> None:
     r, s, secs = spec.split(":")
     if int(r) == rank and int(s) == step:
         print(f"[fault injection] rank {rank} stalls {secs} s before step {step}", file=sys.stderr, flush=True)
+        time.sleep(float(secs))
+
+
+def slow_save() -> None:
+    secs = os.environ.get("IMAGENT_FAULT_SLOW_SAVE")
+    if secs:
+        print(f"[fault injection] checkpoint write stalls {secs} s", file=sys.stderr, flush=True)
         time.sleep(float(secs))

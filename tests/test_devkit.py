@@ -69,3 +69,54 @@ def test_devkit_and_archives_give_the_torchvision_layout(tmp_path):
     assert tuple(x.shape) == (6, 6, 3) and y == 1
     # second construction: layout already in place, nothing re-extracted
     assert len(ImageNetU8(str(tmp_path), "val", (6, 6))) == 5
+
+
+def _prep_worker(rank, root, outdir):
+    from imagent_amd.data.devkit import prepare
+    for split in ("train", "val"):
+        prepare(root, split)
+    open(os.path.join(outdir, f"ok{rank}"), "w").close()
+
+
+def test_concurrent_ranks_prepare_once(tmp_path):
+    """every rank calls prepare() at once (no rank gating in the engine); the file
+    lock lets one do the work and the others find the finished layout."""
+    pytest.importorskip("scipy")
+    import torch.multiprocessing as mp
+    from imagent_amd.data.imagenet import ImageNetU8
+    root = tmp_path / "in"
+    root.mkdir()
+    wnids, gt = _make(str(root))
+    mp.start_processes(_prep_worker, args=(str(root), str(tmp_path)), nprocs=3, start_method="spawn", join=True)
+    assert all(os.path.exists(tmp_path / f"ok{r}") for r in range(3))
+    val = ImageNetU8(str(root), "val", (6, 6))
+    assert len(val) == 5 and sorted(os.listdir(root / "val")) == sorted(set(wnids))
+    assert len(ImageNetU8(str(root), "train", (6, 6))) == 6
+    assert not any(n.endswith(".partial") for n in os.listdir(root))
+
+
+def test_interrupted_val_sort_resumes_from_its_plan(tmp_path):
+    """A sort interrupted after some moves resumes from the written plan: the remaining flat
+    files keep the class that their position in the ORIGINAL sorted listing gives them."""
+    pytest.importorskip("scipy")
+    import json
+    import tarfile as tf
+    from imagent_amd.data.devkit import prepare
+    from imagent_amd.data.imagenet import ImageNetU8
+    wnids, gt = _make(str(tmp_path))
+    prepare(str(tmp_path), "train")  # writes meta.bin
+    d = tmp_path / "val"
+    d.mkdir()
+    with tf.open(tmp_path / "ILSVRC2012_img_val.tar") as t:
+        t.extractall(d)
+    names = sorted(os.listdir(d))
+    plan = [[n, wnids[g - 1]] for n, g in zip(names, gt)]
+    (d / ".sort_plan.json").write_text(json.dumps(plan))
+    for n, w in plan[:2]:  # the first two moves happened before the "crash"
+        (d / w).mkdir(exist_ok=True)
+        os.rename(d / n, d / w / n)
+    prepare(str(tmp_path), "val")
+    assert not (d / ".sort_plan.json").exists()
+    got = {os.path.basename(p): y for p, y in ImageNetU8(str(tmp_path), "val", (6, 6)).samples}
+    for k, g in enumerate(gt):
+        assert got[f"ILSVRC2012_val_{k + 1:08d}.JPEG"] == g - 1

@@ -94,3 +94,21 @@ def test_watchdog_ends_a_hung_two_rank_job(tmp_path):
     assert "[watchdog rank 0] no progress for 4 s" in r.stdout, r.stdout[-3000:]
     assert "exitcode  : 75" in r.stdout or "exit code 75" in r.stdout or "exitcode: 75" in r.stdout, r.stdout[-2000:]
     assert dt < 60, dt
+
+
+@pytest.mark.slow
+def test_slow_checkpoint_write_does_not_trip_the_watchdog(tmp_path):
+    """the master writes its checkpoint for longer than --step-timeout while the other
+    rank waits; both watchdogs are disarmed around the write and the ranks meet in a barrier
+    afterwards, so the healthy job completes (no exit 75)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", IMAGENT_FAULT_SLOW_SAVE="7")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29541", "-m", "imagent_amd.cli"] + COMMON + \
+          ["--epochs", "2", "--backend", "gloo", "--tb-dir", "", "--step-timeout", "3", "--save-model",
+           "--checkpoint-dir", str(tmp_path)]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "[fault injection] checkpoint write stalls 7 s" in r.stdout
+    assert "no progress" not in r.stdout, r.stdout[-3000:]
+    assert r.stdout.count("Epoch 2 Summary: ") == 1
