@@ -56,6 +56,12 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 #define IMK_EXPORT extern "C" __attribute__((visibility("default")))
 
+// host-side count of conv kernel launches (conv_igemm.hip): lets the per-call conv log
+// (ops/conv.py IMAGENT_CONV_LOG) map each call to its kernel dispatches in a rocprof trace
+// (scripts/conv_roofline.py)
+extern "C" int g_imk_conv_launches;
+#define CONV_COUNTED() (++g_imk_conv_launches)
+
 #define IMK_CHECK_LAUNCH()                         \
     do {                                           \
         hipError_t e_ = hipGetLastError();         \

@@ -353,6 +353,7 @@ int launch_halo(const IGemmArgs& a, hipStream_t st) {
         return e ? atoi(e) : 0;
     }();
     hipLaunchKernelGGL((halo3x3_kernel<W, R, EPI>), dim3(G), dim3(512), lds, st, a, nbands, dbg);
+    CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -2,42 +2,22 @@
 // Kernels, layout and design notes: conv_igemm_impl.h; fp8: conv_igemm_fp8.hip.
 
 #include "conv_igemm_impl.h"
-#include "conv_pingpong.h"
+#include "conv_igemm_v3.h"
 
-// Tile selection: Nout <= 64 -> 128x64 (1x4 waves), else 128x128 (2x2 waves).
-// IMAGENT_IGEMM_V2=1: the phased kernel (igemm_dma2_kernel, also explicit tile 10)
-// for the staged-epilogue 256x256 tiles. Measured SLOWER than the single-barrier
-// ring at every R50 shape (256@14 3x3: 426-530 vs 362 us; profiles/
-// r50_conv_phased_kernel.md), so off by default.
-static bool dma2_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("IMAGENT_IGEMM_V2");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
+// Tile selection (auto, tile 0):
+//  * 64 -> 64 3x3 stride 1: the halo-tiled kernel (conv_halo.hip);
+//  * 1x1 with C in {64, 128, 256, 512}: the streaming kernel (conv_stream.hip);
+//  * C % 64 == 0 with the staged epilogue (every long-K conv, every fused BN-backward dgrad):
+//    the v3 main loop (conv_igemm_v3.h), 256x256 tiles for Nout >= 512, else 128x128
+//    (round-3 A/B at R50 / 1024 img, profiles/r50_b1024_conv_v3.md);
+//  * the rest (C % 64 != 0, direct epilogues, Nout <= 64): the LDS-DMA ring / register-staged
+//    kernels of conv_igemm_impl.h.
+// Explicit tiles (A/B, tests): 1-9 ring / register-staged variants, 17 / 18 v3 256x256 / 128x128.
+// Measured slower and removed in round 3: the phased 256x256 kernel (profiles/
+// r50_conv_phased_kernel.md), the ping-pong 256x256 kernel after the 8-phase template (-3.2 %),
+// static wave priority for the second half of the waves (neutral).
 
-// IMAGENT_IGEMM_PP (A/B): the ping-pong 256x256 kernel (conv_pingpong.h) in place of the
-// 2-stage ring for the auto-selected 256x256 tiles with C % 64 == 0: 1 = waves 4-7 staggered
-// by half a phase, 2 = not staggered, 0 = off. Explicit tiles 11 / 12 force it.
-static int igemm_pp() {
-    static const int v = [] {
-        const char* e = getenv("IMAGENT_IGEMM_PP");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
-// IMAGENT_IGEMM_PRIO (A/B): wave priority scheme of the staged-epilogue 256x256 tiles
-static int igemm_prio() {
-    static const int v = [] {
-        const char* e = getenv("IMAGENT_IGEMM_PRIO");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-
-// Wave-quantisation tail of the one-tile-per-block 256x256 kernel (one block per CU): with
+// Wave-quantisation tail of the one-tile-per-block 256x256 kernels (one block per CU): with
 // T tiles on S CUs the last of ceil(T / S) rounds runs T mod S tiles on an otherwise idle chip
 // (R50 at 1024 img: 784 tiles on 256 CUs = 3 rounds + 16 tiles for every N = 256 conv at 14x14).
 // When that remainder is a small fraction of S, the conv is split at an IMAGE boundary: the
@@ -102,6 +82,9 @@ static void advance_images(IGemmArgs& t, const IGemmArgs& a, int i1) {
     if (a.bny) t.bny = a.bny + i1 * ys;
     if (a.bnx2) t.bnx2 = a.bnx2 + i1 * ys;
 }
+
+extern "C" int g_imk_conv_launches = 0;
+IMK_EXPORT int imk_conv_launches() { return g_imk_conv_launches; }
 
 IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     const IGemmArgs& a = *args;
@@ -168,13 +151,25 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
-    if (tile == 11 || tile == 12) {  // ping-pong 256x256 kernel: staged epilogue, C % 64 == 0
-        if (!lds_ok || md != 0) return -105;
-        return tile == 11 ? launch_pp<true>(a, st) : launch_pp<false>(a, st);
+    if (tile == 17 || tile == 18) {  // v3 main loop (conv_igemm_v3.h)
+        if (!use_lds || !v3_ok(a)) return -105;
+        return tile == 17 ? launch_v3<256, 256, 2, 2, 8, 128>(a, st) : launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
-    if (tile == 10) {  // phased 256x256 kernel: staged epilogue only
-        if (!lds_ok) return -105;
-        return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
+    if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
+        const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+        if (a.Nout >= 512 && t8 >= 192) {
+            const int i1 = tail_split_images(a);
+            if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles
+                IGemmArgs m = a, t = a;
+                m.N = i1;
+                m.M = i1 * a.OH * a.OW;
+                advance_images(t, a, i1);
+                const int r = launch_v3<256, 256, 2, 2, 8, 128>(m, st);
+                return r != 0 ? r : launch_v3<128, 128, 2, 2, 4, 128>(t, st);
+            }
+            return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+        }
+        return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
     if (bnb || use_lds) {  // the tiles the auto choice makes, with a fused / staged epilogue
         if (regstage || (tile != 2 && tile != 8)) {
@@ -188,14 +183,6 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
 #define IG_DB(BM_, BN_, WN_, NS_, NW_, E_)                                                  \
     (md == 0 ? launch_dma<BM_, BN_, WN_, NS_, 0, NW_, E_>(a, st)                       \
              : launch_dma<BM_, BN_, WN_, NS_, 1, NW_, E_>(a, st))
-        if (use_lds && tile == 8 && dma2_enabled()) return md == 0 ? launch_dma2<0>(a, st) : launch_dma2<1>(a, st);
-        if (use_lds && tile == 8 && igemm_prio() == 0)
-            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 0>(a, st)
-                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 0>(a, st);
-        if (use_lds && tile == 8 && igemm_prio() == 2)
-            return md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2, 2, 0, 2>(a, st)
-                           : launch_dma<256, 256, 2, 2, 1, 8, 2, 2, 0, 2>(a, st);
-        const int pp = (use_lds && tile == 8 && autotile && md == 0) ? igemm_pp() : 0;
         if (use_lds && tile == 8 && autotile) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {
@@ -203,16 +190,12 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
                 m.N = i1;
                 m.M = i1 * a.OH * a.OW;
                 advance_images(t, a, i1);
-                const int r = pp == 1   ? launch_pp<true>(m, st)
-                              : pp == 2 ? launch_pp<false>(m, st)
-                              : md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2>(m, st)
-                                        : launch_dma<256, 256, 2, 2, 1, 8, 2>(m, st);
+                const int r = md == 0 ? launch_dma<256, 256, 2, 2, 0, 8, 2>(m, st)
+                                      : launch_dma<256, 256, 2, 2, 1, 8, 2>(m, st);
                 if (r != 0) return r;
                 return md == 0 ? launch_dma<128, 128, 2, 2, 0, 4, 2>(t, st) : launch_dma<128, 128, 2, 2, 1, 4, 2>(t, st);
             }
         }
-        if (pp == 1) return launch_pp<true>(a, st);
-        if (pp == 2) return launch_pp<false>(a, st);
         if (use_lds) return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 2) : IG_DB(128, 128, 2, 2, 4, 2);
         return tile == 8 ? IG_DB(256, 256, 2, 2, 8, 1) : IG_DB(128, 128, 2, 2, 4, 1);
 #undef IG_DB

@@ -596,19 +596,36 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
     }
 }
 
-// MFMA over one 64-deep stage held in LDS (rows of 128 B, chunk-swizzled)
-template <int FN, int FM>
+// LDS row swizzle of the stage ring: the 16-B chunk a lane's fragment read or DMA
+// write lands in is the logical chunk XOR swz(row).
+//  * 128-B rows (BK = 64): swz = row & 7 -- the 8 rows of a ds_read_b128 lane group
+//    cover all 8 chunk columns of the 256-B bank row;
+//  * 64-B rows (BK = 32): a 256-B bank row holds 4 rows (bank group = 16 (row & 3) +
+//    4 chunk), and a ds_read_b128 lane group {0-3,12-15,20-27} (and the three others,
+//    MI355X_MICROARCH.md LDS table) takes row blocks {0,3} at logical chunk g and {1,2}
+//    at g ^ 1: swz = h[(row >> 2) & 3] with h = {0, 2, 3, 1} gives all 16 bank groups
+//    distinct physical chunks in every lane group -> conflict-free.
+template <int RB>
+__device__ __forceinline__ int lds_swz(int row) {
+    if (RB == 128) return row & 7;
+    return (120 >> (2 * ((row >> 2) & 3))) & 3;
+}
+
+// MFMA over one stage held in LDS (rows of RB bytes = RB / 64 k-steps of 32,
+// chunk-swizzled); fk[ks] = element offset of the lane's 16-B chunk in k-step ks
+template <int FN, int FM, int RB = 128>
 __device__ __forceinline__ void mfma_stage(f32x4 (&acc)[FN][FM], const bf16_t* bx, const bf16_t* bw, int fk0,
                                            int fk1) {
+    constexpr int LDKE = RB / 2;  // row pitch in elements
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    for (int ks = 0; ks < RB / 64; ++ks) {
         bf16x8 fw[FN], fx[FM];
 #pragma unroll
         for (int i = 0; i < FN; ++i)
-            fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + (ks ? fk1 : fk0));
+            fw[i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDKE + (ks ? fk1 : fk0));
 #pragma unroll
         for (int j = 0; j < FM; ++j)
-            fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDK + (ks ? fk1 : fk0));
+            fx[j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDKE + (ks ? fk1 : fk0));
 #pragma unroll
         for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -653,24 +670,30 @@ __device__ __forceinline__ void mfma_stage_fp8(f32x4 (&acc)[FN][FM], const char*
 // EB = operand element bytes: 2 (bf16, 64-deep stages) or 1 (fp8 e4m3, 128-deep
 // stages, IG_FP8): the DMA moves 16-B chunks either way, the gather differs
 // only in elements per chunk.
-// PRIO: 1 (default) = s_setprio(1) around each stage's MFMAs (256@14 3x3 fwd 366 -> 357 us,
-// 512@7 3x3 337 -> 320 us, bench +0.9 %), 0 = none, 2 = static priority 1 for the second half
-// of the waves (MI355X_MICROARCH.md "Two waves per SIMD", item 4: neutral here)
+// s_setprio(1) around each stage's MFMAs (256@14 3x3 fwd 366 -> 357 us, 512@7 3x3 337 -> 320 us,
+// bench +0.9 %; static priority for the second half of the waves, MI355X_MICROARCH.md "Two waves
+// per SIMD" item 4, measured neutral and removed)
+// RB: LDS row bytes = K bytes per stage (128: BK 64 bf16; 64: BK 32 bf16, twice the stages in
+// the same LDS -> more stages in flight for the 256x256 tile, whose 64-KiB BK-64 stages allow
+// only a 2-deep ring in 160 KiB).
 template <int BM, int BN, int WN, int NS, int MODE, int NW, int EPI, int EB = 2, int FB = 0,
-          int PRIO = 1>  // MODE 0: one tap/stage
+          int RB = 128>  // MODE 0: one tap/stage
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 16, FN = TN / 16;
-    constexpr int QA = BM / (8 * NW), QB = BN / (8 * NW);  // DMA pieces (8 rows each) per wave per stage
+    constexpr int RPP = 1024 / RB;             // rows per DMA piece (64 lanes x 16 B)
+    constexpr int CPR = RB / 16;               // 16-B chunks per row
+    constexpr int QA = BM / (RPP * NW), QB = BN / (RPP * NW);  // DMA pieces per wave per stage
     static_assert(QA >= 1 && QB >= 1 && WM * WN == NW, "tile / wave split");
+    static_assert(RB == 128 || (RB == 64 && EB == 2), "64-B rows: bf16 only");
     constexpr int LPS = QA + QB;               // vmcnt units per stage
-    constexpr int KS = 128 / EB;               // k elements per stage (one 128-B LDS row)
+    constexpr int KS = RB / EB;                // k elements per stage (one LDS row)
     constexpr int CE = 16 / EB;                // elements per 16-B chunk
-    constexpr int SAB = BM * 128, SBB = BN * 128;  // bytes per stage buffer
+    constexpr int SAB = BM * RB, SBB = BN * RB;  // bytes per stage buffer
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* sX = smem;                 // [NS][BM][128 B]
-    char* sW = smem + NS * SAB;      // [NS][BN][128 B]
+    char* sX = smem;                 // [NS][BM][RB]
+    char* sW = smem + NS * SAB;      // [NS][BN][RB]
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -686,10 +709,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     const int nk = max(1, (K + KS - 1) / KS);
     const int nstages = my_tiles * nk;
     const int ohw = a.OH * a.OW;
-    // this lane's DMA slot: row (lane>>3) of each 8-row piece, physical chunk
-    // lane&7 -> logical chunk (lane&7) ^ (row & 7)   (row & 7 == lane >> 3)
-    const int lrow = lane >> 3;
-    const int lchunk = (lane & 7) ^ lrow;
+    // this lane's DMA slot: row lane / CPR of each RPP-row piece, physical chunk
+    // lane % CPR -> logical chunk (lane % CPR) ^ swz(row) (pieces start at multiples of RPP)
+    const int lrow = lane / CPR;
+    const int lchunk = (lane % CPR) ^ lds_swz<RB>(lrow);
     const char* zero = reinterpret_cast<const char*>(g_igemm_zero);
     const char* Xb = reinterpret_cast<const char*>(a.X);
     const char* Wb = reinterpret_cast<const char*>(a.Wk);
@@ -704,7 +727,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         const int m0 = (tile / nbn) * BM, n0 = (tile % nbn) * BN;
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
-            const int m = m0 + (wid * QA + q) * 8 + lrow;
+            const int m = m0 + (wid * QA + q) * RPP + lrow;
             mok[q] = m < a.M;
             const int mm = mok[q] ? m : 0;
             const int img = mm / ohw, rem = mm - img * ohw;
@@ -715,7 +738,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         }
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
-            const int n = n0 + (wid * QB + q) * 8 + lrow;
+            const int n = n0 + (wid * QB + q) * RPP + lrow;
             nok[q] = n < a.Nout;
             wrow[q] = Wb + (size_t)(nok[q] ? n : 0) * a.ldb * EB;
         }
@@ -775,10 +798,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
     };
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p) issue_next();
-    if (PRIO == 2 && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
     const int fr = lane & 15;
-    const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
+    // fragment rows are 16-row aligned + fr, so swz(row) == swz(fr)
+    const int fk0 = (((lane >> 4) + 0) ^ lds_swz<RB>(fr)) * 8, fk1 = (((lane >> 4) + 4) ^ lds_swz<RB>(fr)) * 8;
     // fp8: the lane's 32 bytes are logical chunks 2g, 2g+1 of its row (byte offsets)
     const int f8c0 = ((2 * (lane >> 4)) ^ (fr & 7)) * 16, f8c1 = ((2 * (lane >> 4) + 1) ^ (fr & 7)) * 16;
     const int sx8 = EB == 1 ? 127 + a.xexp[0] : 127, sw8 = EB == 1 ? 127 + a.wexp[0] : 127;
@@ -798,10 +821,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
             mfma_stage_fp8<FN, FM, FB>(acc, sX + buf * SAB + (wm * TM + fr) * 128, sW + buf * SBB + (wn * TN + fr) * 128,
                                    f8c0, f8c1, sw8, sx8);
         else {
-            if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
-            mfma_stage<FN, FM>(acc, reinterpret_cast<const bf16_t*>(sX + buf * SAB) + (wm * TM + fr) * LDK,
-                               reinterpret_cast<const bf16_t*>(sW + buf * SBB) + (wn * TN + fr) * LDK, fk0, fk1);
-            if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(1);
+            mfma_stage<FN, FM, RB>(acc, reinterpret_cast<const bf16_t*>(sX + buf * SAB + (wm * TM + fr) * RB),
+                                   reinterpret_cast<const bf16_t*>(sW + buf * SBB + (wn * TN + fr) * RB), fk0, fk1);
+            __builtin_amdgcn_s_setprio(0);
         }
         if (++kt == nk) {
             const int tile = lid + tj * G;
@@ -821,236 +844,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_dma_kernel(con
         const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
         epilogue_lds<BM, BN, NW * 64, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st);
     }
-}
-
-// ==================================================== phased LDS-DMA kernel (v2)
-// 256 x 256 tile, 8 waves as 2 (pixels) x 4 (channels), one tile per block (long-K
-// convs, staged epilogue). Every 64-deep K-tile is computed in 4 PHASES: phase q
-// multiplies the wave's pixel quarter q (32 pixels) by its 64 channels over K 64
-// (16 MFMAs). The two K-tile buffers ([2][256][128 B] pixels, [2][256][128 B]
-// weights) are filled by LDS-DMA at quarter / part granularity, so loads run
-// several phases ahead instead of one whole K-tile:
-//  * phase (t, q) issues pixel quarter q of K-tile t+1 (1 DMA per wave) into the
-//    slot last read in phase (t-1, q);
-//  * a K-tile's weights are read into registers once, in its phase 0, so their
-//    slot is free from phase (t, 1): phases (t, 1..3) issue the weights of K-tile
-//    t+2 (2 + 1 + 1 DMAs per wave).
-// Pixel quarters land 4 phases and weights 5-7 phases before their first read.
-// Each phase ends with a COUNTED vmcnt that retires exactly what the next phase
-// reads (positions tracked in issue order), then a raw s_barrier: no vmcnt(0) in
-// the loop (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4).
-__device__ __forceinline__ void wait_vm_upto(int n) {
-#define WV2(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
-    switch (n) {
-        case 0: WV2(0); break;
-        case 1: WV2(1); break;
-        case 2: WV2(2); break;
-        case 3: WV2(3); break;
-        case 4: WV2(4); break;
-        case 5: WV2(5); break;
-        case 6: WV2(6); break;
-        case 7: WV2(7); break;
-        case 8: WV2(8); break;
-        case 9: WV2(9); break;
-        case 10: WV2(10); break;
-        case 11: WV2(11); break;
-        default: WV2(0); break;  // (more in flight than any schedule issues: be safe)
-    }
-#undef WV2
-}
-
-// PH phases per K-tile (2 or 4); PRIO: s_setprio(1) around each phase's MFMAs
-template <int MODE, int PH = 4, bool PRIO = false>  // MODE 0: C % 64 == 0 (one tap per K-tile), 1: per-lane
-__global__ __launch_bounds__(512, 1) void igemm_dma2_kernel(const IGemmArgs a) {
-    constexpr int BM = 256, BN = 256;
-    constexpr int FN = 4, FM = 8;  // per wave: 64 channels x 128 pixels
-    constexpr int QPH = 4 / PH;    // pixel quarters per phase
-    constexpr int FPH = FM / PH;   // pixel fragments per phase
-    constexpr int SAB = BM * 128, SBB = BN * 128;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* sX = smem;            // [2][BM][128 B]
-    char* sW = smem + 2 * SAB;  // [2][BN][128 B]
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid >> 2, wc = wid & 3;
-    const int nbn = (a.Nout + BN - 1) / BN;
-    const int nbm = (a.M + BM - 1) / BM;
-    const int lid = xcd_remap(blockIdx.x, gridDim.x);
-    if (lid >= nbm * nbn) return;
-    const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
-    const int K = a.nth * a.ntw * a.C;
-    const int nk = max(1, (K + 63) / 64);
-    const int ohw = a.OH * a.OW;
-    const int lrow = lane >> 3;
-    const int lchunk = (lane & 7) ^ lrow;  // source-side swizzle: LDS image stays lane-linear
-    const char* zero = reinterpret_cast<const char*>(g_igemm_zero);
-    const char* Xb = reinterpret_cast<const char*>(a.X);
-    const char* Wb = reinterpret_cast<const char*>(a.Wk);
-
-    // pixel rows this lane DMAs: quarter q -> tile row xr0(q) + lrow
-    const char* xrow[4];
-    int ih0[4], iw0[4];
-    bool mok[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int m = m0 + (wid >> 2) * 128 + q * 32 + (wid & 3) * 8 + lrow;
-        mok[q] = m < a.M;
-        const int mm = mok[q] ? m : 0;
-        const int img = mm / ohw, rem = mm - img * ohw;
-        const int oh = rem / a.OW, ow = rem - oh * a.OW;
-        xrow[q] = Xb + (size_t)img * a.H * a.W * a.C * 2;
-        ih0[q] = oh * a.sA;
-        iw0[q] = ow * a.sA;
-    }
-    // weight rows: part j -> tile row wid * 32 + j * 8 + lrow
-    const char* wrow[4];
-    bool nok[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wid * 32 + j * 8 + lrow;
-        nok[j] = n < a.Nout;
-        wrow[j] = Wb + (size_t)(nok[j] ? n : 0) * a.ldb * 2;
-    }
-    struct Tap {
-        int dh, dw, wtap, c;
-        bool kok;
-    };
-    auto tap_of = [&](int kt) {
-        Tap r;
-        int t;
-        const int k = kt * 64 + lchunk * 8;
-        if (MODE == 0) {
-            t = (kt * 64) / a.C;
-            r.c = kt * 64 - t * a.C + lchunk * 8;
-        } else {
-            t = k / a.C;
-            r.c = k - t * a.C;
-        }
-        r.kok = k < K;
-        const int ti = r.kok ? t / a.ntw : 0, tj = r.kok ? t - ti * a.ntw : 0;
-        r.dh = a.dh0 + ti * a.dhs;
-        r.dw = a.dw0 + tj * a.dws;
-        r.wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
-        return r;
-    };
-    auto issue_x = [&](int kt, int q) {
-        const Tap tp = tap_of(kt);
-        const int ih = ih0[q] + tp.dh, iw = iw0[q] + tp.dw;
-        const bool ok = tp.kok && mok[q] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        const char* src = ok ? xrow[q] + (((size_t)ih * a.W + iw) * a.C + tp.c) * 2 : zero;
-        char* dst = sX + (kt & 1) * SAB + ((wid >> 2) * 128 + q * 32 + (wid & 3) * 8) * 128;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-    };
-    auto issue_w = [&](int kt, int j) {
-        const Tap tp = tap_of(kt);
-        const char* src = (tp.kok && nok[j]) ? wrow[j] + ((size_t)tp.wtap * a.C + tp.c) * 2 : zero;
-        char* dst = sW + (kt & 1) * SBB + (wid * 32 + j * 8) * 128;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                         (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-    };
-
-    f32x4 acc[FN][FM];
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * ((a.flags & IG_BNBWD) ? 3 : 2) * a.Nout
-                        : nullptr;
-
-    // issue positions (this wave's DMA count after each item) of what later phases read:
-    // posA[q] = pixel quarter q of the K-tile being read next, posB[b] = weights in buffer b
-    int issued = 0, posA[4] = {0, 0, 0, 0}, posB[2] = {0, 0};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) issue_w(0, j);
-    issued += 4;
-    posB[0] = issued;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        issue_x(0, q);
-        posA[q] = ++issued;
-    }
-    if (nk > 1) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) issue_w(1, j);
-        issued += 4;
-        posB[1] = issued;
-    }
-    wait_vm_upto(issued - max(posA[QPH - 1], posB[0]));
-    __builtin_amdgcn_s_barrier();
-
-    const int fr = lane & 15;
-    const int fk0 = (((lane >> 4) + 0) ^ (fr & 7)) * 8, fk1 = (((lane >> 4) + 4) ^ (fr & 7)) * 8;
-    for (int t = 0; t < nk; ++t) {
-        const int buf = t & 1;
-        const bf16_t* bx = reinterpret_cast<const bf16_t*>(sX + buf * SAB) + (wr * 128 + fr) * LDK;
-        const bf16_t* bw = reinterpret_cast<const bf16_t*>(sW + buf * SBB) + (wc * 64 + fr) * LDK;
-        bf16x8 fw[2][FN];
-#pragma unroll
-        for (int h = 0; h < PH; ++h) {
-            // ---- operands: the K-tile's weights once, this phase's pixel rows
-            if (h == 0) {
-#pragma unroll
-                for (int i = 0; i < FN; ++i) {
-                    fw[0][i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + fk0);
-                    fw[1][i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDK + fk1);
-                }
-            }
-            bf16x8 fx[2][FPH];
-#pragma unroll
-            for (int jj = 0; jj < FPH; ++jj) {
-                fx[0][jj] = *reinterpret_cast<const bf16x8*>(bx + (h * FPH * 16 + jj * 16) * LDK + fk0);
-                fx[1][jj] = *reinterpret_cast<const bf16x8*>(bx + (h * FPH * 16 + jj * 16) * LDK + fk1);
-            }
-            // ---- issue into slots whose last reads retired before the previous barrier
-            if (t + 1 < nk) {
-#pragma unroll
-                for (int u = 0; u < QPH; ++u) {
-                    issue_x(t + 1, h * QPH + u);
-                    posA[h * QPH + u] = ++issued;
-                }
-            }
-            if (t + 2 < nk) {
-                if (PH == 2 && h == 1) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) issue_w(t + 2, j);
-                    issued += 4;
-                    posB[buf] = issued;
-                } else if (PH == 4 && h >= 1) {
-                    if (h == 1) {
-                        issue_w(t + 2, 0);
-                        issue_w(t + 2, 1);
-                        issued += 2;
-                    } else {
-                        issue_w(t + 2, h);
-                        issued += 1;
-                    }
-                    if (h == 3) posB[buf] = issued;
-                }
-            }
-            if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                for (int i = 0; i < FN; ++i)
-#pragma unroll
-                    for (int jj = 0; jj < FPH; ++jj)
-                        acc[i][h * FPH + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            fw[ks][i], fx[ks][jj], acc[i][h * FPH + jj], 0, 0, 0);
-            if (PRIO) __builtin_amdgcn_s_setprio(0);
-            // ---- retire exactly what the next phase reads, then the barrier
-            if (!(t == nk - 1 && h == PH - 1)) {
-                int need;
-                if (h == PH - 1) need = max(posA[QPH - 1], posB[buf ^ 1]);  // next K-tile: first rows + weights
-                else need = posA[(h + 2) * QPH - 1];                       // this K-tile: next rows
-                wait_vm_upto(issued - need);
-            }
-            __builtin_amdgcn_s_barrier();
-        }
-    }
-    __syncthreads();  // every DMA retired; the ring becomes the epilogue's staging area
-    epilogue_lds<BM, BN, 512, FN, FM>(a, acc, smem, m0, n0, wr * 128, wc * 64, lane, tid, st);
 }
 
 // ================================================= register-staged kernel
@@ -1247,17 +1040,19 @@ inline int grid_size(int ntiles, int nk, int resident) {
     return (nk > 4 || ntiles < resident) ? ntiles : resident;
 }
 
-template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0, int PRIO = 1>
+template <int BM, int BN, int WN, int NS, int MD, int NW = 4, int EPI = 0, int EB = 2, int FB = 0,
+          int RB = 128>
 int launch_dma(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-    size_t lds = (size_t)NS * (BM + BN) * 128;
+    size_t lds = (size_t)NS * (BM + BN) * RB;
     if (EPI == 2) lds = std::max(lds, epi_lds_bytes(BM, BN, NW * 64));
     static int resident = 0;
     if (resident == 0)
-        resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, PRIO>, lds, NW * 64);
-    const int nk = (a.nth * a.ntw * a.C * EB + 127) / 128;
-    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, PRIO>),
+        resident = resident_blocks(igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, RB>, lds, NW * 64);
+    const int nk = (a.nth * a.ntw * a.C * EB + RB - 1) / RB;
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WN, NS, MD, NW, EPI, EB, FB, RB>),
                        dim3(EPI == 2 ? ntiles : grid_size(ntiles, nk, resident)), dim3(NW * 64), lds, st, a);
+    CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -1273,32 +1068,9 @@ int launch_rs(const IGemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((igemm_rs_kernel<BM, BN, WN, MD, EPI>),
                        dim3(EPI == 2 ? ntiles : grid_size(ntiles, (K + BK - 1) / BK, resident)),
                        dim3(256), lds, st, a);
+    CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
-}
-
-template <int MD, int PH, bool PRIO>
-int launch_dma2v(const IGemmArgs& a, hipStream_t st) {
-    const int ntiles = ((a.M + 255) / 256) * ((a.Nout + 255) / 256);
-    const size_t lds = std::max((size_t)2 * (256 + 256) * 128, epi_lds_bytes(256, 256, 512));
-    hipLaunchKernelGGL((igemm_dma2_kernel<MD, PH, PRIO>), dim3(ntiles), dim3(512), lds, st, a);
-    IMK_CHECK_LAUNCH();
-    return 0;
-}
-
-// IMAGENT_IGEMM_V2_VARIANT: 0 = 4 phases, 1 = 4 phases + setprio, 2 = 2 phases, 3 = 2 phases + setprio
-template <int MD>
-int launch_dma2(const IGemmArgs& a, hipStream_t st) {
-    static const int v = [] {
-        const char* e = getenv("IMAGENT_IGEMM_V2_VARIANT");
-        return e ? atoi(e) : 3;
-    }();
-    switch (v) {
-        case 0: return launch_dma2v<MD, 4, false>(a, st);
-        case 1: return launch_dma2v<MD, 4, true>(a, st);
-        case 2: return launch_dma2v<MD, 2, false>(a, st);
-        default: return launch_dma2v<MD, 2, true>(a, st);
-    }
 }
 
 }  // namespace

@@ -1,0 +1,233 @@
+// Implicit-GEMM conv main loop v3 for gfx950 (MI355X): the long-K convs with C % 64 == 0
+// (every 3x3 and the K >= 256 1x1 convs of ResNet; cuDNN's conv fwd / dgrad in the reference,
+// /root/reference/imagenet.py:312, forward :123, backward :128).
+//
+// Same gather-GEMM formulation, LDS ring (128-B rows, XOR-swizzled 16-B chunks, LDS-DMA fills)
+// and staged epilogue as igemm_dma_kernel (conv_igemm_impl.h). What changed is the cost of a
+// stage, measured by the main-loop decomposition of round 3 (scripts/dbg_mainloop.sh: the
+// 128x128 ring on 256@14 3x3 took 335 us, of which the loop skeleton alone -- barriers,
+// per-stage gather bookkeeping, epilogue -- was 102 us, the DMA path 165 us and the MFMA
+// path 118 us, nearly additive):
+//
+//  * DMA addressing through BUFFER descriptors (buffer_load_dwordx4 ... lds): one 32-bit
+//    per-lane offset per 8-row piece, recomputed only when the filter TAP changes (3 VALU),
+//    the within-tap channel advance in the wave-uniform soffset (SALU), and out-of-image
+//    taps / rows beyond M or Nout as an out-of-range offset that the buffer unit returns as
+//    zeros (no zero line, no per-stage 64-bit address arithmetic, no per-stage division:
+//    the tap index is tracked incrementally).
+//  * Fragment reads software-pipelined: a stage's MFMAs run in half-k-step groups
+//    (FN/2 x FM MFMAs) and each group's LDS reads are issued one group ahead, so the MFMA
+//    chain no longer stops on s_waitcnt lgkmcnt(0) after every 8 MFMAs
+//    (sched_group_barrier pins the DS-read / MFMA interleave).
+//
+// Out-of-range semantics relied on (raw buffer, stride 0): a lane whose offset is
+// >= num_records reads zeros. Offsets of invalid lanes are OOB_OFF = 2^31 and tensors
+// are < 2^31 bytes (host check), so the lane is out of range whether or not the
+// hardware adds soffset into the check.
+
+#pragma once
+
+#include "conv_igemm_impl.h"
+
+namespace {
+
+constexpr uint32_t OOB_OFF = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t v3_rsrc(const void* p, uint32_t bytes) {
+    // built from kernel arguments only (wave-uniform, cdna_hip_programming.md T20)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void v3_dma(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+// RB: LDS row bytes per stage (128: BK 64; 64: BK 32). NS: ring depth.
+template <int BM, int BN, int WN, int NS, int NW, int RB>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(const IGemmArgs a) {
+    constexpr int WM = NW / WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    constexpr int RPP = 1024 / RB, CPR = RB / 16;
+    constexpr int QA = BM / (RPP * NW), QB = BN / (RPP * NW);
+    static_assert(QA >= 1 && QB >= 1 && WM * WN == NW && FN % 2 == 0, "tile / wave split");
+    constexpr int LPS = QA + QB;
+    constexpr int KS = RB / 2;        // k (bf16) per stage
+    constexpr int NKS = RB / 64;      // MFMA k-steps (32) per stage
+    constexpr int SAB = BM * RB, SBB = BN * RB;
+    constexpr int FH = FN / 2;        // channel fragments per half group
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sX = smem;
+    char* sW = smem + NS * SAB;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wid % WN, wm = wid / WN;
+    const int nbn = (a.Nout + BN - 1) / BN;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    if (lid >= ((a.M + BM - 1) / BM) * nbn) return;
+    const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
+    const int ntaps = a.nth * a.ntw;
+    const int cps = a.C / KS;          // stages per tap (C % 64 == 0, host)
+    const int nk = ntaps * cps;
+    const int ohw = a.OH * a.OW;
+    const int lrow = lane / CPR;
+    const int lchunk = (lane % CPR) ^ lds_swz<RB>(lrow);
+    const __amdgpu_buffer_rsrc_t rx = v3_rsrc(a.X, (uint32_t)((size_t)a.N * a.H * a.W * a.C * 2));
+    const __amdgpu_buffer_rsrc_t rw = v3_rsrc(a.Wk, (uint32_t)((size_t)a.Nout * a.ldb * 2));
+
+    // per X piece: byte offset of (img, ih0, iw0, lchunk) -- may be "negative" (a border pixel's
+    // first tap), only valid taps' offsets are ever used -- and the valid-tap bit mask
+    int64_t xbase[QA];
+    uint32_t xmask[QA];
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+        const int m = m0 + (wid * QA + q) * RPP + lrow;
+        const bool mok = m < a.M;
+        const int mm = mok ? m : 0;
+        const int img = mm / ohw, rem = mm - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const int ih0 = oh * a.sA + a.dh0, iw0 = ow * a.sA + a.dw0;
+        xbase[q] = (((int64_t)img * a.H + ih0) * a.W + iw0) * a.C * 2 + lchunk * 16;
+        uint32_t mk = 0;
+        for (int ti = 0; ti < a.nth; ++ti) {
+            const int ih = ih0 + ti * a.dhs;
+            for (int tj = 0; tj < a.ntw; ++tj) {
+                const int iw = iw0 + tj * a.dws;
+                if (mok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) mk |= 1u << (ti * a.ntw + tj);
+            }
+        }
+        xmask[q] = mk;
+    }
+    uint32_t vw[QB];
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+        const int n = n0 + (wid * QB + q) * RPP + lrow;
+        vw[q] = n < a.Nout ? (uint32_t)(n * a.ldb * 2 + lchunk * 16) : OOB_OFF;
+    }
+
+    // issue cursor: tap (ti, tj) = t, channel stage cs within the tap
+    int it = 0, iti = 0, itj = 0, ics = 0, is = 0;
+    uint32_t vx[QA];
+    int xtap = 0, wtap = 0;  // uniform: byte offset of the tap in X, weight column of the tap
+    auto set_tap = [&]() {
+        const int dh = iti * a.dhs, dw = itj * a.dws;
+        xtap = (dh * a.W + dw) * a.C * 2;
+        wtap = ((a.kh0 + iti * a.khs) * a.KW + (a.kw0 + itj * a.kws)) * a.C * 2;
+#pragma unroll
+        for (int q = 0; q < QA; ++q)
+            vx[q] = (xmask[q] >> it) & 1 ? (uint32_t)(xbase[q] + xtap) : OOB_OFF;
+    };
+    auto issue_next = [&]() {
+        if (is >= nk) return;
+        const int buf = is % NS;
+        char* dX = sX + buf * SAB + (wid * QA) * 1024;
+        char* dW = sW + buf * SBB + (wid * QB) * 1024;
+        const uint32_t cso = (uint32_t)(ics * RB);
+#pragma unroll
+        for (int q = 0; q < QA; ++q) v3_dma(rx, dX + q * 1024, vx[q], cso);
+#pragma unroll
+        for (int q = 0; q < QB; ++q) v3_dma(rw, dW + q * 1024, vw[q], (uint32_t)wtap + cso);
+        ++is;
+        if (++ics == cps) {
+            ics = 0;
+            ++it;
+            if (++itj == a.ntw) {
+                itj = 0;
+                ++iti;
+            }
+            if (it < ntaps) set_tap();
+        }
+    };
+    set_tap();
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue_next();
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float* st = a.stats ? a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * ((a.flags & IG_BNBWD) ? 3 : 2) * a.Nout
+                        : nullptr;
+
+    const int fr = lane & 15;
+    constexpr int LDKE = RB / 2;
+    int fk[2];
+    fk[0] = (((lane >> 4) + 0) ^ lds_swz<RB>(fr)) * 8;
+    fk[1] = (((lane >> 4) + 4) ^ lds_swz<RB>(fr)) * 8;
+    for (int s = 0; s < nk; ++s) {
+        if (is - 1 - s >= NS - 2)
+            __builtin_amdgcn_s_waitcnt((((NS - 2) * LPS) & 0xF) | ((((NS - 2) * LPS) >> 4) << 14) | (0x7 << 4) |
+                                       (0xF << 8));
+        else
+            __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        __builtin_amdgcn_s_barrier();
+        issue_next();
+        const int buf = s % NS;
+        const bf16_t* bx = reinterpret_cast<const bf16_t*>(sX + buf * SAB + (wm * TM + fr) * RB);
+        const bf16_t* bw = reinterpret_cast<const bf16_t*>(sW + buf * SBB + (wn * TN + fr) * RB);
+        // groups g = (ks, h): h = 0 reads the k-step's pixel fragments + channel half 0, h = 1
+        // channel half 1; each group's reads are issued before the previous group's MFMAs
+        bf16x8 fx[2][FM], fw[2][FH];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) fx[0][j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDKE + fk[0]);
+#pragma unroll
+        for (int i = 0; i < FH; ++i) fw[0][i] = *reinterpret_cast<const bf16x8*>(bw + i * 16 * LDKE + fk[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, FM + FH, 0);  // group 0's reads first
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int g = 0; g < 2 * NKS; ++g) {
+            const int ks = g >> 1, h = g & 1;
+            const int xs = ks & 1, ws = g & 1;  // register sets of this group
+            if (g + 1 < 2 * NKS) {  // prefetch group g + 1
+                const int ks1 = (g + 1) >> 1, h1 = (g + 1) & 1;
+                if (h1 == 0) {
+#pragma unroll
+                    for (int j = 0; j < FM; ++j)
+                        fx[ks1 & 1][j] = *reinterpret_cast<const bf16x8*>(bx + j * 16 * LDKE + fk[ks1]);
+                }
+#pragma unroll
+                for (int i = 0; i < FH; ++i)
+                    fw[ws ^ 1][i] =
+                        *reinterpret_cast<const bf16x8*>(bw + (h1 * FH + i) * 16 * LDKE + fk[ks1]);
+                if (h1 == 0)
+                    __builtin_amdgcn_sched_group_barrier(0x100, FM + FH, 0);  // DS reads
+                else
+                    __builtin_amdgcn_sched_group_barrier(0x100, FH, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < FH; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j)
+                    acc[h * FH + i][j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ws][i], fx[xs][j], acc[h * FH + i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x8, FH * FM, 0);  // MFMAs
+        }
+        __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();  // every DMA retired (last wait) and every wave done reading: the ring is free
+    epilogue_lds<BM, BN, NW * 64, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st);
+}
+
+template <int BM, int BN, int WN, int NS, int NW, int RB>
+int launch_v3(const IGemmArgs& a, hipStream_t st) {
+    const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+    const size_t lds = std::max((size_t)NS * (BM + BN) * RB, epi_lds_bytes(BM, BN, NW * 64));
+    hipLaunchKernelGGL((igemm_v3_kernel<BM, BN, WN, NS, NW, RB>), dim3(ntiles), dim3(NW * 64), lds, st, a);
+    CONV_COUNTED();
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// shapes v3 covers: C % 64 == 0 (one tap per stage), taps <= 32, operands < 2^31 bytes, and the staged
+// (bf16, no bias / ReLU) epilogue
+inline bool v3_ok(const IGemmArgs& a) {
+    if (a.C % 64 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
+    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_FP8 | IG_AFFINE)) return false;
+    if (a.bias || a.xbn || a.X2 || a.Nout % 8 || a.ldy % 8) return false;
+    const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
+    return xb < (1ull << 31) && wb < (1ull << 31);
+}
+
+}  // namespace

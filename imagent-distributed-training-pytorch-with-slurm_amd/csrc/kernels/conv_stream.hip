@@ -376,6 +376,7 @@ int launch_stream1(const IGemmArgs& a, hipStream_t st) {
     // enough pixel blocks to fill the chip, but >= D groups per wave
     const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
     hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM, XBN>), dim3(npb * nsl), dim3(256), lds, st, a);
+    CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
 }

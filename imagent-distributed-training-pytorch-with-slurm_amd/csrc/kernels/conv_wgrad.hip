@@ -321,6 +321,7 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
     hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR, XF, XB>), dim3(ntiles * splits), dim3(NW * 64), lds,
                        st, a);
+    CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -135,6 +135,7 @@ def _declare(name: str, lib) -> None:
         sigs = {
             "imk_conv_igemm": [C.POINTER(IGemmArgs), i32, vp],
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
+            "imk_conv_launches": [],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
                            vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],

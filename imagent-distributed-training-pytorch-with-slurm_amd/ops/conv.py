@@ -36,6 +36,47 @@ def _magic(d: int) -> Tuple[int, int]:
     return m & 0xFFFFFFFF, s
 
 
+# IMAGENT_CONV_LOG=<path>: append one JSON line per conv kernel call (op, GEMM shape, flags, kernel
+# dispatches it produced, stream) -- joined with a rocprofv3 kernel trace by scripts/conv_roofline.py
+_LOG_PATH = os.environ.get("IMAGENT_CONV_LOG")
+_log_file = None
+
+
+def _igemm_call(a, tile: int, st, what: str) -> None:
+    k = _lib.kernels()
+    if _LOG_PATH is None:
+        _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), what)
+        return
+    n0 = k.imk_conv_launches()
+    _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), what)
+    _log(dict(op=what, N=a.N, H=a.H, W=a.W, C=a.C, OH=a.OH, OW=a.OW, M=a.M, Nout=a.Nout, taps=a.nth * a.ntw,
+              YH=a.YH, YW=a.YW, sY=a.sY, ldy=a.ldy, flags=a.flags, bnb=bool(a.flags & 32), y2=bool(a.bny),
+              x2=bool(a.bnx2), stats=bool(a.stats), xbn=bool(a.xbn), X2=bool(a.X2)),
+         k.imk_conv_launches() - n0, st)
+
+
+def _wgrad_call(a, splits: int, st, what: str) -> None:
+    k = _lib.kernels()
+    if _LOG_PATH is None:
+        _lib.check(k.imk_conv_wgrad(C.byref(a), splits, st), what)
+        return
+    n0 = k.imk_conv_launches()
+    _lib.check(k.imk_conv_wgrad(C.byref(a), splits, st), what)
+    _log(dict(op=what, N=a.N, H=a.H, W=a.W, C=a.Ci, Co=a.Co, OH=a.OH, OW=a.OW, M=a.M, KH=a.KH, KW=a.KW,
+              stride=a.stride, stem=bool(a.stem), xbn=bool(a.xbn)), k.imk_conv_launches() - n0, st)
+
+
+def _log(rec, nk: int, st) -> None:
+    global _log_file
+    import json
+    if _log_file is None:
+        _log_file = open(_LOG_PATH, "a")
+    rec["kernels"] = nk
+    rec["stream"] = int(st or 0)
+    _log_file.write(json.dumps(rec) + "\n")
+    _log_file.flush()
+
+
 def _base_args(x_ptr, w_ptr, y_ptr, N, H, W, Cin, OH, OW, Nout, ldb, sA) -> _lib.IGemmArgs:
     a = _lib.IGemmArgs()
     a.X, a.Wk, a.Y = x_ptr, w_ptr, y_ptr
@@ -124,7 +165,7 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
                 a.shift = stats.save.data_ptr()
             stats = stats.slab
         a.stats = stats.data_ptr()
-    _lib.check(_lib.kernels().imk_conv_igemm(C.byref(a), tile, _lib.stream_ptr()), "conv fwd")
+    _igemm_call(a, tile, _lib.stream_ptr(), "conv fwd")
     return out
 
 
@@ -199,7 +240,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
                 (4096 if (accumulate and old_sub2) else 0)
             if bnb is not None:
                 bnb.fill(a)
-            _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), "conv dgrad")
+            _igemm_call(a, tile, st, "conv dgrad")
     return out
 
 
@@ -249,7 +290,7 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     if xbn is not None:
         assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
         a.xbn = xbn.data_ptr()
-    _lib.check(_lib.kernels().imk_conv_wgrad(C.byref(a), splits, _lib.stream_ptr()), "conv wgrad")
+    _wgrad_call(a, splits, _lib.stream_ptr(), "conv wgrad")
 
 
 def bnfold_ok(conv, g: torch.Tensor, bnb: Optional["BNBwdFuse"]) -> bool:
@@ -286,7 +327,7 @@ def igemm_dgrad_bnfold(g: torch.Tensor, x: torch.Tensor, coef: torch.Tensor, con
     a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, 1, 0, 0, Ci
     a.flags = 0
     bnb.fill(a)
-    _lib.check(k.imk_conv_igemm(C.byref(a), 0, st), "conv dgrad (folded BN backward)")
+    _igemm_call(a, 0, st, "conv dgrad (folded BN backward)")
     return out
 
 
@@ -310,7 +351,7 @@ def conv_wgrad_bnfold(mod, g: torch.Tensor, x: torch.Tensor, coef: torch.Tensor,
         a.m_per_split = 0
         a.mg_ohw, a.sh_ohw = _magic(OH * OW)
         a.mg_ow, a.sh_ow = _magic(OW)
-        _lib.check(_lib.kernels().imk_conv_wgrad(C.byref(a), 0, _lib.stream_ptr()), "conv wgrad (folded BN)")
+        _wgrad_call(a, 0, _lib.stream_ptr(), "conv wgrad (folded BN)")
         notify_ready(mod.weight)
     if side is not None:
         streams.protect(g, x, coef, h)

@@ -131,12 +131,27 @@ def main():
             r["fp8_fwd_us"] = t8
             tot["fp8_fwd"] += t8 * cnt
         if a.tiles and not stem:
+            yref = igemm_fwd(x, w, s, p, k, k).float()
+            dref = igemm_dgrad(dy, wt, (H, H), s, p, k, k).float()
+
+            def rel(u, v):
+                return float((u.float() - v).norm() / v.norm().clamp_min(1e-30))
             for t in (int(v) for v in a.tiles.split(",")):
-                tf = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, tile=t))
-                td = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, tile=t))
+                try:
+                    ef = rel(igemm_fwd(x, w, s, p, k, k, tile=t), yref)
+                    ed = rel(igemm_dgrad(dy, wt, (H, H), s, p, k, k, tile=t), dref)
+                    tf = timeit(lambda: igemm_fwd(x, w, s, p, k, k, stats=stats, tile=t))
+                    td = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, tile=t))
+                except RuntimeError as e:  # a tile that does not cover this shape
+                    line += f"\n      tile {t}: n/a ({str(e)[:60]})"
+                    continue
                 line += f"\n      tile {t}: fwd {tf:8.1f} us {flops / tf / 1e6:6.0f} TF | dgrad {td:8.1f} us " \
-                        f"{flops / td / 1e6:6.0f} TF"
-                r[f"tile{t}"] = (tf, td)
+                        f"{flops / td / 1e6:6.0f} TF | rel err vs auto fwd {ef:.1e} dgrad {ed:.1e}"
+                r[f"tile{t}"] = (tf, td, ef, ed)
+                if ef > 2e-2 or ed > 2e-2:
+                    line += "  <-- MISMATCH"
+                tot[f"tile{t}_fwd"] += tf * cnt
+                tot[f"tile{t}_dgrad"] += td * cnt
         print(line, flush=True)
         rows.append(r)
         tot["fwd"] += t_f * cnt
