@@ -96,11 +96,10 @@ def main(argv=None):
                          "forward + loss + top-k counters, imagenet.py:166-210) and report val_img_s")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
                     help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward; fp32: the reference's own "
-                         "precision (imagenet.py:312 trains fp32), PyTorch/MIOpen path only (--kernels torch)")
+                         "precision (imagenet.py:312 trains fp32): exact-f32 MFMA kernels with --kernels hip "
+                         "(models/native_f32.py), PyTorch/MIOpen with --kernels torch")
     a = ap.parse_args(argv)
-    if a.dtype == "fp32" and a.kernels != "torch":
-        raise SystemExit("--dtype fp32 runs on the PyTorch/MIOpen path: add --kernels torch (the HIP kernels are "
-                         "bf16 / fp8 MFMA)")
+    f32_hip = a.dtype == "fp32" and a.kernels == "hip"
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and "SLURM_PROCID" not in os.environ:
         raise SystemExit(_self_launch(argv))
 
@@ -163,7 +162,11 @@ def main(argv=None):
         model = resnet.build(a.arch)
         order = list(reversed(range(len(list(model.parameters())))))
         native = None
-        if a.kernels == "hip":
+        if f32_hip:
+            from imagent_amd.models.native_f32 import bind_native_f32
+            native = bind_native_f32(model, dev, order)
+            arena = native.arena
+        elif a.kernels == "hip":
             from imagent_amd.models.native import bind_native
             native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8",
                                  wgrad_overlap=bool(a.wgrad_overlap))
@@ -184,13 +187,14 @@ def main(argv=None):
         else:
             opt = FlatSGD(arena, lr=0.1, momentum=0.9, weight_decay=1e-4, after_step=after)
         metrics = DeviceMetrics(dev)
-        runner = StepRunner(ddp, opt, metrics, a.kernels, 0.0,
+        runner = StepRunner(ddp, opt, metrics, "hip_f32" if f32_hip else a.kernels, 0.0,
                             torch.bfloat16 if (a.kernels == "torch" and a.dtype == "bf16") else None)
         if a.kernels == "torch":
             model.to(memory_format=torch.channels_last)
         src = SyntheticImageNet(a.batch_size * 4, a.image_size, 1000, a.batch_size, dev, seed=0,
                                 rank=ctx.rank)
-        tf = InputTransform(a.kernels, (a.image_size, a.image_size), cpad=resnet.ResNet.STEM_CPAD)
+        tf = InputTransform("hip_f32" if f32_hip else a.kernels, (a.image_size, a.image_size),
+                            cpad=resnet.ResNet.STEM_CPAD)
         model.train()
 
         def one(u8, y):
@@ -253,6 +257,8 @@ def main(argv=None):
                 "vs_baseline": round(value / base, 3) if base else None,
                 "dtype": ("fp32" if (not on_gpu or a.dtype == "fp32") else "bf16" if a.dtype == "bf16" else
                           "fp8 (e4m3 forward convs, bf16 backward)"),
+                "fp32_kernels": ("own exact-f32 MFMA kernels" if f32_hip else "PyTorch/MIOpen")
+                if a.dtype == "fp32" else None,
                 "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
                         "random-init weights)",
                 "config": {
@@ -275,7 +281,7 @@ def main(argv=None):
                     "world_size": ctx.world_size,
                     "comm_nranks": getattr(comm, "nranks", comm.world_size),
                     "collectives_per_step": coll_per_step,
-                    "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip",
+                    "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip" and not f32_hip,
                     "auto_batch_reduced": auto_reduced,
                     "bucket_mb": a.bucket_mb,
                     "mean_train_loss": round(loss, 4),

@@ -1,0 +1,718 @@
+// fp32 training path for gfx950 (MI355X): the reference's own precision.
+//
+// The reference trains ResNet-18 at 448x448 in fp32 with no AMP (/root/reference/imagenet.py:281
+// Resize(448), :312 resnet18, :442 batch 128). These kernels run that configuration on
+// this framework's own code at fp32 accuracy (tests: <= 1e-4 relative against PyTorch fp32):
+//
+//  * igemm_f32_kernel: the same gather-GEMM formulation as the bf16 convs (IGemmArgs: forward,
+//    stride-1 dgrad, each parity class of a strided dgrad, the 4-channel stem, the FC layer) on
+//    the exact-f32 MFMA v_mfma_f32_16x16x4_f32 (one f32 operand per lane, fp32 accumulate; 1/16 of
+//    the bf16 MFMA rate, MI355X_MICROARCH.md "Matrix cores"). The operand k order inside a 16-deep
+//    LDS chunk is permuted identically for both operands (lane group g feeds k = 4g + s at sub-step
+//    s), so every lane reads its 4 k-values with one ds_read_b128 from the same 128-B-row,
+//    row-XOR-swizzled LDS image the bf16 kernels use. Register-staged double buffer, 128x128 tile,
+//    2 blocks per CU: the MFMA pipe, not the operand path, is the limit at this rate.
+//  * wgrad_f32_kernel: dW[co][k] += sum_m dY[m][co] X_gather[m][k], split over m with fp32
+//    atomics into dW; both operands staged as [m][col] rows (pitch 144 floats: the two row
+//    groups of a ds_read_b32 half-wave land 16 banks apart) and read transposed.
+//  * BatchNorm (training statistics as per-block partial slabs folded in a fixed order ->
+//    deterministic; apply with residual add + ReLU; backward reduce + apply), maxpool with
+//    argmax, global average pool, FC bias column sums, input normalisation to fp32.
+
+#include "conv_igemm_impl.h"
+
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ conv fwd / dgrad
+constexpr int F_BM = 128, F_BN = 128, F_BK = 32;  // BK in floats: one 128-B LDS row
+
+template <int MODE>  // 0: C % 32 == 0 (one tap per stage), 1: per-chunk tap (C % 4 == 0)
+__global__ __launch_bounds__(256, 2) void igemm_f32_kernel(const IGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* sX = reinterpret_cast<float*>(smem);          // [2][BM][32]
+    float* sW = sX + 2 * F_BM * F_BK;                    // [2][BN][32]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wn = wid & 1, wm = wid >> 1;               // 2 x 2 waves, 64 x 64 each
+    const int nbn = (a.Nout + F_BN - 1) / F_BN;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    if (lid >= ((a.M + F_BM - 1) / F_BM) * nbn) return;
+    const int m0 = (lid / nbn) * F_BM, n0 = (lid % nbn) * F_BN;
+    const int K = a.nth * a.ntw * a.C;
+    const int nk = (K + F_BK - 1) / F_BK;
+    const int ohw = a.OH * a.OW;
+    const int col8 = tid & 7;  // this thread's 16-B chunk (4 k) of a staged row
+    const float* X = reinterpret_cast<const float*>(a.X);
+    const float* Wk = reinterpret_cast<const float*>(a.Wk);
+
+    const float* xrow[4];
+    int ih0[4], iw0[4];
+    bool mok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + (tid >> 3) + 32 * i;
+        mok[i] = m < a.M;
+        const int mm = mok[i] ? m : 0;
+        const int img = mm / ohw, rem = mm - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        xrow[i] = X + (size_t)img * a.H * a.W * a.C;
+        ih0[i] = oh * a.sA;
+        iw0[i] = ow * a.sA;
+    }
+    const float* wrow[4];
+    bool nok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + (tid >> 3) + 32 * j;
+        nok[j] = n < a.Nout;
+        wrow[j] = Wk + (size_t)(nok[j] ? n : 0) * a.ldb;
+    }
+    f32x4v rx[4], rw[4];
+    auto load = [&](int kt) {
+        const int k = kt * F_BK + col8 * 4;
+        int t, c;
+        if (MODE == 0) {
+            t = (kt * F_BK) / a.C;
+            c = kt * F_BK - t * a.C + col8 * 4;
+        } else {
+            t = k / a.C;
+            c = k - t * a.C;
+        }
+        const bool kok = k < K;
+        const int ti = kok ? t / a.ntw : 0, tj = kok ? t - ti * a.ntw : 0;
+        const int dh = a.dh0 + ti * a.dhs, dw = a.dw0 + tj * a.dws;
+        const int wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ih = ih0[i] + dh, iw = iw0[i] + dw;
+            const bool ok = kok && mok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+            rx[i] = ok ? *reinterpret_cast<const f32x4v*>(xrow[i] + ((size_t)ih * a.W + iw) * a.C + c)
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            rw[j] = (kok && nok[j]) ? *reinterpret_cast<const f32x4v*>(wrow[j] + (size_t)wtap * a.C + c)
+                                    : f32x4v{0.f, 0.f, 0.f, 0.f};
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = (tid >> 3) + 32 * i;
+            *reinterpret_cast<f32x4v*>(sX + (buf * F_BM + r) * F_BK + ((col8 ^ (r & 7)) * 4)) = rx[i];
+            *reinterpret_cast<f32x4v*>(sW + (buf * F_BN + r) * F_BK + ((col8 ^ (r & 7)) * 4)) = rw[i];
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load(0);
+    store(0);
+    __syncthreads();
+    const int fr = lane & 15, g = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load(kt + 1);
+        const float* bx = sX + (buf * F_BM + wm * 64 + fr) * F_BK;
+        const float* bw = sW + (buf * F_BN + wn * 64 + fr) * F_BK;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int off = ((ks * 4 + g) ^ (fr & 7)) * 4;  // fragment rows are 16-aligned + fr
+            f32x4v fw[4], fx[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fw[i] = *reinterpret_cast<const f32x4v*>(bw + i * 16 * F_BK + off);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) fx[j] = *reinterpret_cast<const f32x4v*>(bx + j * 16 * F_BK + off);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fw[i][s], fx[j][s], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) {
+            __syncthreads();  // everyone is done reading buf ^ 1 (iteration kt - 1)
+            store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // epilogue: lane holds channels nb + i*16 + 4g + r of pixel mb + j*16 + fr
+    const bool accum = a.flags & IG_ACCUM;
+    const float* bias = a.bias;
+    float* Y = reinterpret_cast<float*>(a.Y);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + fr;
+        if (m >= a.M) continue;
+        const int img = m / ohw, rem = m - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        float* yp = Y + (((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = n0 + wn * 64 + i * 16 + 4 * g;
+            f32x4 v = acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (bias && n + r < a.Nout) v[r] += bias[n + r];
+            if (n + 3 < a.Nout && (a.ldy & 3) == 0) {
+                f32x4* p = reinterpret_cast<f32x4*>(yp + n);
+                if (accum) v += *p;
+                *p = v;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < a.Nout) yp[n + r] = accum ? yp[n + r] + v[r] : v[r];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ wgrad
+struct WgradF32Args {
+    const float* dY;  // [M][Co] (output grid NHWC)
+    const float* X;   // [N][H][W][C]
+    float* dW;        // [Co][KH][KW][C] (+=)
+    int N, H, W, C, Co, OH, OW, M, KH, KW, stride, pad, m_per_split;
+};
+
+constexpr int WG_M = 32;      // pixels per stage
+constexpr int WG_P = 144;     // LDS row pitch (floats)
+
+template <int BCO, int BK>
+__global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a) {
+    constexpr int WCO = BCO == 128 ? 2 : 1, WK = 4 / WCO;  // 4 waves
+    constexpr int TCO = BCO / WCO, TK = BK / WK;           // wave tile
+    constexpr int FI = TCO / 16, FJ = TK / 16;
+    constexpr int CA = WG_M * BCO / 4 / 256, CB = WG_M * BK / 4 / 256;  // 16-B chunks per thread per stage
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* sA = reinterpret_cast<float*>(smem);   // [2][WG_M][WG_P] dY
+    float* sB = sA + 2 * WG_M * WG_P;             // [2][WG_M][WG_P] X gather
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wc = wid % WCO, wk = wid / WCO;
+    const int Kt = a.KH * a.KW * a.C;
+    const int nco = (a.Co + BCO - 1) / BCO, nkt = (Kt + BK - 1) / BK;
+    const int tile = blockIdx.x % (nco * nkt), split = blockIdx.x / (nco * nkt);
+    const int co0 = (tile % nco) * BCO, k0 = (tile / nco) * BK;
+    const int mbeg = split * a.m_per_split, mend = min(a.M, mbeg + a.m_per_split);
+    if (mbeg >= mend) return;
+    const int ohw = a.OH * a.OW;
+    // chunk assignment: A chunk q -> (row = q / (BCO/4), col4 = q % (BCO/4)); same for B with BK
+    f32x4v ra[CA], rb[CB];
+    auto load = [&](int mb) {
+#pragma unroll
+        for (int u = 0; u < CA; ++u) {
+            const int q = tid + 256 * u;
+            const int r = q / (BCO / 4), cc = (q % (BCO / 4)) * 4;
+            const int m = mb + r, co = co0 + cc;
+            ra[u] = (m < mend && co < a.Co) ? *reinterpret_cast<const f32x4v*>(a.dY + (size_t)m * a.Co + co)
+                                            : f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int q = tid + 256 * u;
+            const int r = q / (BK / 4), kc = (q % (BK / 4)) * 4;
+            const int m = mb + r, k = k0 + kc;
+            f32x4v v = {0.f, 0.f, 0.f, 0.f};
+            if (m < mend && k < Kt) {
+                const int t = k / a.C, c = k - t * a.C;
+                const int kh = t / a.KW, kw = t - kh * a.KW;
+                const int img = m / ohw, rem = m - img * ohw;
+                const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                    v = *reinterpret_cast<const f32x4v*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.C + c);
+            }
+            rb[u] = v;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < CA; ++u) {
+            const int q = tid + 256 * u;
+            *reinterpret_cast<f32x4v*>(sA + (buf * WG_M + q / (BCO / 4)) * WG_P + (q % (BCO / 4)) * 4) = ra[u];
+        }
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int q = tid + 256 * u;
+            *reinterpret_cast<f32x4v*>(sB + (buf * WG_M + q / (BK / 4)) * WG_P + (q % (BK / 4)) * 4) = rb[u];
+        }
+    };
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nst = (mend - mbeg + WG_M - 1) / WG_M;
+    load(mbeg);
+    store(0);
+    __syncthreads();
+    const int fr = lane & 15, g = lane >> 4;
+    for (int s = 0; s < nst; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nst) load(mbeg + (s + 1) * WG_M);
+        const float* ba = sA + buf * WG_M * WG_P + wc * TCO + fr;
+        const float* bb = sB + buf * WG_M * WG_P + wk * TK + fr;
+#pragma unroll
+        for (int t = 0; t < WG_M / 4; ++t) {  // instruction t: lane group g feeds pixel 4t + g
+            float fa[FI], fb[FJ];
+#pragma unroll
+            for (int i = 0; i < FI; ++i) fa[i] = ba[(4 * t + g) * WG_P + i * 16];
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) fb[j] = bb[(4 * t + g) * WG_P + j * 16];
+#pragma unroll
+            for (int i = 0; i < FI; ++i)
+#pragma unroll
+                for (int j = 0; j < FJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (s + 1 < nst) {
+            __syncthreads();
+            store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // lane: rows (co) co0 + wc*TCO + i*16 + 4g + r, column (k) k0 + wk*TK + j*16 + fr
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int k = k0 + wk * TK + j * 16 + fr;
+            if (k >= Kt) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + wc * TCO + i * 16 + 4 * g + r;
+                if (co < a.Co) atomicAdd(a.dW + (size_t)co * Kt + k, acc[i][j][r]);
+            }
+        }
+}
+
+// ------------------------------------------------------------------ BatchNorm
+// Partial sums per block over rows [r0, r1): slab[blk][q][C], q = 0: sum(v - s), 1: sum((v - s)^2)
+// (forward; s = shift[c]) or q = 0: sum(g'), 1: sum(g' * xhat) (backward; g' = g masked by y > 0).
+// Thread layout: C/4 threads per row (f32x4), 256 / (C/4) rows per pass.
+constexpr int BN_MAXB = 1024;
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_partial_f32_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ stat,  // shift | mean,rstd
+                                                             float* __restrict__ slab, long R, int C) {
+    const int cpr = C / 4, rpb = 256 / cpr, tid = threadIdx.x;
+    const int ch = tid % cpr, c0 = ch * 4;
+    const bool active = tid < rpb * cpr;
+    f32x4v s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, sh = s1, rs = s1;
+    if (active) {
+        sh = *reinterpret_cast<const f32x4v*>(stat + c0);
+        if (BWD) rs = *reinterpret_cast<const f32x4v*>(stat + C + c0);
+    }
+    const long rows_per_blk = (R + gridDim.x - 1) / gridDim.x;
+    const long r0 = (long)blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+    if (active)
+        for (long r = r0 + tid / cpr; r < r1; r += rpb) {
+            const size_t off = (size_t)r * C + c0;
+            const f32x4v xv = *reinterpret_cast<const f32x4v*>(x + off);
+            if (!BWD) {
+                const f32x4v d = xv - sh;
+                s1 += d;
+                s2 += d * d;
+            } else {
+                f32x4v gv = *reinterpret_cast<const f32x4v*>(g + off);
+                if (y) {
+                    const f32x4v yv = *reinterpret_cast<const f32x4v*>(y + off);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (!(yv[q] > 0.f)) gv[q] = 0.f;
+                }
+                s1 += gv;
+                s2 += gv * ((xv - sh) * rs);
+            }
+        }
+    __shared__ float red[2][256 * 4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        red[0][tid * 4 + q] = s1[q];
+        red[1][tid * 4 + q] = s2[q];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {  // fixed-order fold over the rows of this block
+        const int cc = c / 4, q = c % 4;
+        float a1 = 0.f, a2 = 0.f;
+        for (int rr = 0; rr < rpb; ++rr) {
+            a1 += red[0][(rr * cpr + cc) * 4 + q];
+            a2 += red[1][(rr * cpr + cc) * 4 + q];
+        }
+        slab[((size_t)blockIdx.x * 2 + 0) * C + c] = a1;
+        slab[((size_t)blockIdx.x * 2 + 1) * C + c] = a2;
+    }
+}
+
+// forward fold: save[0..C) = mean, save[C..2C) = rstd; running stats (momentum, unbiased var)
+__global__ void bn_fold_fwd_f32_kernel(const float* __restrict__ slab, int nb, const float* __restrict__ shift,
+                                       float* __restrict__ save, float* __restrict__ rmean,
+                                       float* __restrict__ rvar, long R, int C, float eps, float momentum) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a1 = 0.0, a2 = 0.0;  // fold of the per-block fp32 partials, fixed order
+    for (int b = 0; b < nb; ++b) {
+        a1 += slab[((size_t)b * 2) * C + c];
+        a2 += slab[((size_t)b * 2 + 1) * C + c];
+    }
+    const double md = a1 / (double)R;
+    const double var = fmax(a2 / (double)R - md * md, 0.0);
+    const float mean = (float)(md + shift[c]);
+    save[c] = mean;
+    save[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) {
+        rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(var * (double)R / (double)max(1L, R - 1));
+    }
+}
+
+// backward fold: red[0..C) = sum(g'), red[C..2C) = sum(g' xhat); dbeta / dgamma accumulate
+__global__ void bn_fold_bwd_f32_kernel(const float* __restrict__ slab, int nb, float* __restrict__ red,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a1 = 0.0, a2 = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        a1 += slab[((size_t)b * 2) * C + c];
+        a2 += slab[((size_t)b * 2 + 1) * C + c];
+    }
+    red[c] = (float)a1;
+    red[C + c] = (float)a2;
+    if (dbeta) dbeta[c] += (float)a1;
+    if (dgamma) dgamma[c] += (float)a2;
+}
+
+// y = (x - mean) rstd gamma + beta (+ res) (ReLU)
+__global__ __launch_bounds__(256) void bn_apply_f32_kernel(const float* __restrict__ x, const float* __restrict__ save,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ res, float* __restrict__ y,
+                                                           long n4, int C, int relu) {
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < n4; t += (long)gridDim.x * 256) {
+        const int c0 = (int)((t * 4) % C);
+        const f32x4v xv = reinterpret_cast<const f32x4v*>(x)[t];
+        f32x4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = c0 + q;
+            o[q] = (xv[q] - save[c]) * save[C + c] * gamma[c] + beta[c];
+        }
+        if (res) o += reinterpret_cast<const f32x4v*>(res)[t];
+        if (relu)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = fmaxf(o[q], 0.f);
+        reinterpret_cast<f32x4v*>(y)[t] = o;
+    }
+}
+
+// dx = gamma rstd (g' - sum(g')/R - xhat sum(g' xhat)/R); dres = g' (when requested)
+__global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __restrict__ g,
+                                                               const float* __restrict__ y,
+                                                               const float* __restrict__ x,
+                                                               const float* __restrict__ save,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ red, float* __restrict__ dx,
+                                                               float* __restrict__ dres, long n4, int C, float inv) {
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < n4; t += (long)gridDim.x * 256) {
+        const int c0 = (int)((t * 4) % C);
+        f32x4v gv = reinterpret_cast<const f32x4v*>(g)[t];
+        if (y) {
+            const f32x4v yv = reinterpret_cast<const f32x4v*>(y)[t];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (!(yv[q] > 0.f)) gv[q] = 0.f;
+        }
+        if (dres) reinterpret_cast<f32x4v*>(dres)[t] = gv;
+        const f32x4v xv = reinterpret_cast<const f32x4v*>(x)[t];
+        f32x4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = c0 + q;
+            const float rstd = save[C + c];
+            const float xh = (xv[q] - save[c]) * rstd;
+            o[q] = gamma[c] * rstd * (gv[q] - red[c] * inv - xh * red[C + c] * inv);
+        }
+        reinterpret_cast<f32x4v*>(dx)[t] = o;
+    }
+}
+
+// ------------------------------------------------------------------ pooling, FC bias, input
+// maxpool k x k / s / p (k <= 3), NHWC, one thread per output element; idx = argmax window slot
+__global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                          int OH, int OW, int k, int s, int p) {
+    const long total = (long)N * OH * OW * C;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int c = t % C;
+        const long pix = t / C;
+        const int ow = pix % OW, oh = (pix / OW) % OH, n = pix / ((long)OW * OH);
+        float best = -INFINITY;
+        int bi = 0;
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j) {
+                const int ih = oh * s - p + i, iw = ow * s - p + j;
+                if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
+                const float v = x[(((size_t)n * H + ih) * W + iw) * C + c];
+                if (v > best || (v != v && best == best)) {
+                    best = v;
+                    bi = i * k + j;
+                }
+            }
+        y[t] = best;
+        idx[t] = (uint8_t)bi;
+    }
+}
+
+// gather form: dx[n][ih][iw][c] = sum of dy over the windows whose argmax is (ih, iw)
+__global__ __launch_bounds__(256) void maxpool_bwd_f32_kernel(const float* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              float* __restrict__ dx, int N, int H, int W, int C,
+                                                              int OH, int OW, int k, int s, int p) {
+    const long total = (long)N * H * W * C;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int c = t % C;
+        const long pix = t / C;
+        const int iw = pix % W, ih = (pix / W) % H, n = pix / ((long)W * H);
+        float acc = 0.f;
+        // windows (oh, ow) with oh*s - p <= ih <= oh*s - p + k - 1
+        const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(OH - 1, (ih + p) / s);
+        const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(OW - 1, (iw + p) / s);
+        for (int oh = oh_lo; oh <= oh_hi; ++oh)
+            for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+                const int i = ih - (oh * s - p), j = iw - (ow * s - p);
+                if (i < 0 || i >= k || j < 0 || j >= k) continue;
+                const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + c;
+                if (idx[o] == i * k + j) acc += dy[o];
+            }
+        dx[t] = acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int N,
+                                                          int HW, int C) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * C) return;
+    const int n = t / C, c = t % C;
+    float acc = 0.f;
+    for (int i = 0; i < HW; ++i) acc += x[((size_t)n * HW + i) * C + c];
+    y[t] = acc / (float)HW;
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_f32_kernel(const float* __restrict__ dy, float* __restrict__ dx,
+                                                              int N, int HW, int C) {
+    const long total = (long)N * HW * C;
+    const float inv = 1.f / (float)HW;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int c = t % C;
+        const int n = t / ((long)HW * C);
+        dx[t] = dy[(size_t)n * C + c] * inv;
+    }
+}
+
+// out[c] += sum_r x[r][c]  (FC bias gradient), fixed order
+__global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ x, float* __restrict__ out, int R,
+                                                         int C) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) acc += x[(size_t)r * C + c];
+    out[c] += acc;
+}
+
+// uint8 HWC (crop / flip) -> fp32 NHWC with Cp channels (3 real, the rest 0)
+__global__ __launch_bounds__(256) void normalize_f32_kernel(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                            const int* __restrict__ crop,
+                                                            const uint8_t* __restrict__ flip, int B, int Hs, int Ws,
+                                                            int H, int W, int Cp, float m0, float m1, float m2,
+                                                            float is0, float is1, float is2) {
+    const long total = (long)B * H * W;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int w = t % W;
+        const long r = t / W;
+        const int h = r % H;
+        const int b = r / H;
+        const int oy = crop ? crop[2 * b] : 0, ox = crop ? crop[2 * b + 1] : 0;
+        const int sw = (flip && flip[b]) ? (W - 1 - w) : w;
+        const uint8_t* px = in + (((size_t)b * Hs + (h + oy)) * Ws + (sw + ox)) * 3;
+        float* o = out + (size_t)t * Cp;
+        o[0] = ((float)px[0] * (1.f / 255.f) - m0) * is0;
+        o[1] = ((float)px[1] * (1.f / 255.f) - m1) * is1;
+        o[2] = ((float)px[2] * (1.f / 255.f) - m2) * is2;
+        for (int c = 3; c < Cp; ++c) o[c] = 0.f;
+    }
+}
+
+int sgrid(long work) {
+    long b = (work + 255) / 256;
+    return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+int bn_blocks(long R, int C) {
+    const int rpb = 256 / (C / 4);
+    long b = (R + 4L * rpb - 1) / (4L * rpb);  // >= 4 rows per thread
+    return (int)(b < BN_MAXB ? (b > 0 ? b : 1) : BN_MAXB);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
+    const IGemmArgs& a = *args;
+    if (a.M <= 0 || a.Nout <= 0) return 0;
+    if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32))) return -100;
+    const int ntiles = ((a.M + F_BM - 1) / F_BM) * ((a.Nout + F_BN - 1) / F_BN);
+    const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);
+    if (a.C % F_BK == 0)
+        hipLaunchKernelGGL(igemm_f32_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(igemm_f32_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_wgrad_f32(const float* dy, const float* x, float* dw, int N, int H, int W, int C, int Co, int OH,
+                             int OW, int KH, int KW, int stride, int pad, void* stream) {
+    if (C % 4 || Co % 4) return -100;
+    WgradF32Args a{dy, x, dw, N, H, W, C, Co, OH, OW, N * OH * OW, KH, KW, stride, pad, 0};
+    const int Kt = KH * KW * C;
+    const bool small = Co <= 64;
+    const int BCO = small ? 64 : 128, BK = 128;
+    const int tiles = ((Co + BCO - 1) / BCO) * ((Kt + BK - 1) / BK);
+    // enough blocks for 2 per CU, at least 8 pixel stages per split
+    int splits = (512 + tiles - 1) / tiles;
+    const int max_splits = (a.M + 8 * WG_M - 1) / (8 * WG_M);
+    splits = std::max(1, std::min(splits, max_splits));
+    a.m_per_split = ((a.M + splits - 1) / splits + WG_M - 1) / WG_M * WG_M;
+    splits = (a.M + a.m_per_split - 1) / a.m_per_split;
+    const size_t lds = 2 * 2 * WG_M * WG_P * sizeof(float);
+    if (small)
+        hipLaunchKernelGGL((wgrad_f32_kernel<64, 128>), dim3(tiles * splits), dim3(256), lds, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL((wgrad_f32_kernel<128, 128>), dim3(tiles * splits), dim3(256), lds, (hipStream_t)stream,
+                           a);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_slab_floats_f32(int C) { return BN_MAXB * 2 * C; }
+
+// training forward statistics: save <- (mean, rstd); running stats updated when rmean != null.
+// shift: per-channel values near the mean (the previous batch mean) for the shifted sums.
+IMK_EXPORT int imk_bn_stats_f32(const float* x, const float* shift, float* slab, float* save, float* rmean,
+                                float* rvar, long R, int C, float eps, float momentum, void* stream) {
+    if (C % 4 || 256 % (C / 4) || C > 1024) return -100;
+    const int nb = bn_blocks(R, C);
+    hipLaunchKernelGGL((bn_partial_f32_kernel<false>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nullptr,
+                       nullptr, shift, slab, R, C);
+    IMK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_fold_fwd_f32_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, slab, nb, shift,
+                       save, rmean, rvar, R, C, eps, momentum);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_apply_f32(const float* x, const float* save, const float* gamma, const float* beta,
+                                const float* res, float* y, long R, int C, int relu, void* stream) {
+    if (C % 4) return -100;
+    const long n4 = R * C / 4;
+    hipLaunchKernelGGL(bn_apply_f32_kernel, dim3(sgrid(n4)), dim3(256), 0, (hipStream_t)stream, x, save, gamma, beta,
+                       res, y, n4, C, relu);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// backward: g' = g * (y > 0) (y null: no ReLU); red <- (sum g', sum g' xhat); dgamma/dbeta +=;
+// dx = BN backward of g'; dres <- g' (nullable)
+IMK_EXPORT int imk_bn_bwd_f32(const float* g, const float* y, const float* x, const float* save, const float* gamma,
+                              float* slab, float* red, float* dgamma, float* dbeta, float* dx, float* dres, long R,
+                              int C, void* stream) {
+    if (C % 4 || 256 % (C / 4) || C > 1024) return -100;
+    const int nb = bn_blocks(R, C);
+    hipLaunchKernelGGL((bn_partial_f32_kernel<true>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, g, y, save,
+                       slab, R, C);
+    IMK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_fold_bwd_f32_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, slab, nb, red,
+                       dgamma, dbeta, C);
+    IMK_CHECK_LAUNCH();
+    const long n4 = R * C / 4;
+    hipLaunchKernelGGL(bn_bwd_apply_f32_kernel, dim3(sgrid(n4)), dim3(256), 0, (hipStream_t)stream, g, y, x, save,
+                       gamma, red, dx, dres, n4, C, 1.f / (float)R);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_maxpool_f32(const float* x, float* y, void* idx, int N, int H, int W, int C, int OH, int OW, int k,
+                               int s, int p, void* stream) {
+    if (k > 3) return -100;
+    hipLaunchKernelGGL(maxpool_f32_kernel, dim3(sgrid((long)N * OH * OW * C)), dim3(256), 0, (hipStream_t)stream, x,
+                       y, (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_maxpool_bwd_f32(const float* dy, const void* idx, float* dx, int N, int H, int W, int C, int OH,
+                                   int OW, int k, int s, int p, void* stream) {
+    hipLaunchKernelGGL(maxpool_bwd_f32_kernel, dim3(sgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+                       dy, (const uint8_t*)idx, dx, N, H, W, C, OH, OW, k, s, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_avgpool_f32(const float* x, float* y, int N, int HW, int C, void* stream) {
+    hipLaunchKernelGGL(avgpool_f32_kernel, dim3((N * C + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, y, N, HW,
+                       C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_avgpool_bwd_f32(const float* dy, float* dx, int N, int HW, int C, void* stream) {
+    hipLaunchKernelGGL(avgpool_bwd_f32_kernel, dim3(sgrid((long)N * HW * C)), dim3(256), 0, (hipStream_t)stream, dy,
+                       dx, N, HW, C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_colsum_f32(const float* x, float* out, int R, int C, void* stream) {
+    hipLaunchKernelGGL(colsum_f32_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, out, R, C);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_normalize_u8_f32(const void* in, float* out, const int* crop, const void* flip, int B, int Hs,
+                                    int Ws, int H, int W, int Cp, const float* mean, const float* std, void* stream) {
+    hipLaunchKernelGGL(normalize_f32_kernel, dim3(sgrid((long)B * H * W)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)in, out, crop, (const uint8_t*)flip, B, Hs, Ws, H, W, Cp, mean[0], mean[1],
+                       mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2]);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// softmax-xent backward with an fp32 gradient (the bf16 path's imk_xent_bwd rounds dz to bf16)
+namespace {
+__global__ __launch_bounds__(256) void xent_bwd_f32_kernel(const float* __restrict__ logits,
+                                                           const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ gout, float* __restrict__ dz,
+                                                           int B, int NC, float smoothing) {
+    const int row = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= NC) return;
+    const float scale = gout[0] / (float)B;
+    const float p = expf(logits[(size_t)row * NC + i] - lse[row]);
+    const float t = (i == labels[row] ? 1.f - smoothing : 0.f) + smoothing / (float)NC;
+    dz[(size_t)row * NC + i] = (p - t) * scale;
+}
+}  // namespace
+
+IMK_EXPORT int imk_xent_bwd_f32(const float* logits, const int64_t* labels, const float* lse, const float* gout,
+                                float* dz, int B, int NC, float smoothing, void* stream) {
+    hipLaunchKernelGGL(xent_bwd_f32_kernel, dim3((NC + 255) / 256, B), dim3(256), 0, (hipStream_t)stream, logits,
+                       labels, lse, gout, dz, B, NC, smoothing);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}

@@ -42,8 +42,10 @@ class InputTransform:
     def __call__(self, u8: torch.Tensor) -> torch.Tensor:
         B, H, W, _ = u8.shape
         oh, ow = self.size
-        if self.backend == "hip":
+        if self.backend in ("hip", "hip_f32"):
             from ..ops.misc import normalize_u8
+            if self.backend == "hip_f32":  # fp32 NHWC for the fp32 kernel path
+                from ..ops.f32 import normalize_u8_f32 as normalize_u8
             crop = flip = None
             if self.flip:
                 flip = torch.randint(0, 2, (B,), dtype=torch.uint8, device=u8.device)

@@ -16,6 +16,8 @@ Two execution backends share these parameters:
   MI355X kernels (ops/*): MFMA implicit-GEMM convs with BN statistics fused
   into their epilogue, fused BN(+add)(+ReLU), fp32 master weights in a flat
   arena with bf16 shadows.
+* ``backend='hip_f32'`` - NHWC fp32 through the fp32 kernels (models/native_f32.py),
+  the reference's own precision.
 * ``backend='torch'`` - NCHW through stock PyTorch ops: the numerical oracle
   for the kernel tests and the path used on CPU (gloo) runs.
 """
@@ -224,6 +226,9 @@ class ResNet(nn.Module):
         if self.backend == "hip":
             from .native import forward_hip
             return forward_hip(self, x)
+        if self.backend == "hip_f32":
+            from .native_f32 import forward_hip_f32
+            return forward_hip_f32(self, x)
         return self.forward_torch(x)
 
 

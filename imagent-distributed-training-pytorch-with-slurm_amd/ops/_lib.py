@@ -136,6 +136,20 @@ def _declare(name: str, lib) -> None:
             "imk_conv_igemm": [C.POINTER(IGemmArgs), i32, vp],
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
             "imk_conv_launches": [],
+            # fp32 path (f32.hip)
+            "imk_conv_f32": [C.POINTER(IGemmArgs), vp],
+            "imk_wgrad_f32": [vp, vp, vp] + [i32] * 11 + [vp],
+            "imk_bn_slab_floats_f32": [i32],
+            "imk_bn_stats_f32": [vp, vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],
+            "imk_bn_apply_f32": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
+            "imk_bn_bwd_f32": [vp] * 11 + [i64, i32, vp],
+            "imk_maxpool_f32": [vp, vp, vp] + [i32] * 9 + [vp],
+            "imk_maxpool_bwd_f32": [vp, vp, vp] + [i32] * 9 + [vp],
+            "imk_avgpool_f32": [vp, vp, i32, i32, i32, vp],
+            "imk_avgpool_bwd_f32": [vp, vp, i32, i32, i32, vp],
+            "imk_colsum_f32": [vp, vp, i32, i32, vp],
+            "imk_normalize_u8_f32": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+            "imk_xent_bwd_f32": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
                            vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],

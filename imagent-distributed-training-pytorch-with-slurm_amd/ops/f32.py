@@ -1,0 +1,315 @@
+"""fp32 ops on the hand-written kernels of ``csrc/kernels/f32.hip`` -- the reference's own precision.
+
+The reference trains in fp32 (no AMP; ``/root/reference/imagenet.py:312`` model, fwd ``:123``,
+loss ``:124``, bwd ``:128``). These autograd Functions run ResNet training at fp32 accuracy on
+the framework's own kernels: NHWC fp32 activations, convolutions on the exact-f32 MFMA, weight
+gradients written straight into the parameters' slots of the flat gradient arena (then the
+bucketed reducer is notified, as on the bf16 path), BatchNorm with deterministic fixed-order
+statistics. Every op is checked against the PyTorch fp32 op at <= 1e-4 relative
+(``tests/test_f32_gpu.py``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from .conv import _base_args, conv_out_size
+from .grad_sink import notify_ready
+
+
+def _k():
+    return _lib.kernels()
+
+
+# ------------------------------------------------------------------ convolution
+def conv_f32(x: torch.Tensor, wk: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
+             bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+             accumulate: bool = False) -> torch.Tensor:
+    """y[N,OH,OW,Co] (+)= conv(x[N,H,W,Ci], wk[Co][KH][KW][Ci]) (+ bias), fp32 NHWC."""
+    N, H, W, Ci = x.shape
+    Co = wk.shape[0]
+    assert x.dtype == torch.float32 and wk.dtype == torch.float32 and x.is_contiguous() and wk.is_contiguous()
+    OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
+    if out is None:
+        out = torch.empty((N, OH, OW, Co), device=x.device, dtype=torch.float32)
+    a = _base_args(x.data_ptr(), wk.data_ptr(), out.data_ptr(), N, H, W, Ci, OH, OW, Co, KH * KW * Ci, stride)
+    a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = KH, KW, -pad, 1, -pad, 1
+    a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, KW
+    a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = OH, OW, 1, 0, 0, Co
+    a.flags = 1 | (8 if accumulate else 0)
+    if bias is not None:
+        a.bias = bias.data_ptr()
+    _lib.check(_k().imk_conv_f32(C.byref(a), _lib.stream_ptr()), "conv f32")
+    return out
+
+
+def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int, KH: int,
+              KW: int) -> torch.Tensor:
+    """dx[N,H,W,Ci] = dgrad(dy[N,OH,OW,Co], wt[Ci][KH][KW][Co]); strided convs as one launch per output
+    parity class touching only the taps that reach it (the bf16 path's sub-pixel decomposition,
+    ops/conv.py igemm_dgrad)."""
+    N, OH, OW, Co = dy.shape
+    Ci = wt.shape[0]
+    H, W = in_hw
+    out = torch.empty((N, H, W, Ci), device=dy.device, dtype=torch.float32)
+    S = stride
+    if S > 1 and (KH < S or KW < S):
+        out.zero_()  # parity classes no tap reaches stay 0
+    for ph in range(S):
+        for pw in range(S):
+            gh, gw = (H - ph + S - 1) // S, (W - pw + S - 1) // S
+            if gh <= 0 or gw <= 0:
+                continue
+            kh0, kw0 = (ph + pad) % S, (pw + pad) % S
+            nth, ntw = max(0, (KH - kh0 + S - 1) // S), max(0, (KW - kw0 + S - 1) // S)
+            if nth == 0 or ntw == 0:
+                continue
+            a = _base_args(dy.data_ptr(), wt.data_ptr(), out.data_ptr(), N, OH, OW, Co, gh, gw, Ci, KH * KW * Co, 1)
+            a.nth, a.ntw = nth, ntw
+            a.dh0, a.dhs = (ph + pad - kh0) // S, -1
+            a.dw0, a.dws = (pw + pad - kw0) // S, -1
+            a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
+            a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
+            a.flags = 1
+            _lib.check(_k().imk_conv_f32(C.byref(a), _lib.stream_ptr()), "conv dgrad f32")
+    return out
+
+
+def wgrad_f32(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int, KH: int,
+              KW: int) -> None:
+    """dw[Co][KH][KW][Ci] (fp32, contiguous) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci])."""
+    N, H, W, Ci = x.shape
+    _, OH, OW, Co = dy.shape
+    assert dw.dtype == torch.float32 and dw.numel() == Co * KH * KW * Ci
+    _lib.check(_k().imk_wgrad_f32(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, Ci, Co, OH, OW, KH, KW,
+                                  stride, pad, _lib.stream_ptr()), "wgrad f32")
+
+
+def _weight_nhwc(mod, cpad: int = 0) -> torch.Tensor:
+    """The fp32 master weight as [Co][KH][KW][Ci] (its channels-last memory; the stem padded to
+    ``cpad`` input channels)."""
+    w = mod.weight.detach().permute(0, 2, 3, 1)
+    if cpad and cpad != w.shape[-1]:
+        wp = torch.zeros(w.shape[:3] + (cpad,), device=w.device, dtype=torch.float32)
+        wp[..., : w.shape[-1]] = w
+        return wp
+    return w.contiguous()
+
+
+class ConvF32Fn(torch.autograd.Function):
+    """NHWC fp32 conv; the weight gradient lands in the parameter's arena slot (``weight.grad``) and
+    the bucketed reducer is notified, as ``ops.conv.ConvFn`` does on the bf16 path."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mod):
+        wk = _weight_nhwc(mod, x.shape[-1])
+        y = conv_f32(x, wk, mod.stride, mod.padding, mod.kh, mod.kw)
+        ctx.mod = mod
+        ctx.save_for_backward(x, wk)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wk = ctx.saved_tensors
+        mod = ctx.mod
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = wk.permute(3, 1, 2, 0).contiguous()  # [Ci][KH][KW][Co]
+            dx = dgrad_f32(dy, wt, (x.shape[1], x.shape[2]), mod.stride, mod.padding, mod.kh, mod.kw)
+        g = mod.weight.grad.permute(0, 2, 3, 1)  # arena view, [Co][KH][KW][Ci] memory
+        if x.shape[-1] != mod.in_channels:  # stem: 4-channel input, 3-channel weight
+            gp = torch.zeros_like(wk)
+            wgrad_f32(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw)
+            g.add_(gp[..., : mod.in_channels])
+        else:
+            assert g.is_contiguous()
+            wgrad_f32(dy, x, g, mod.stride, mod.padding, mod.kh, mod.kw)
+        notify_ready(mod.weight)
+        return dx, None, None
+
+
+class LinearF32Fn(torch.autograd.Function):
+    """fc: x [B, Cin] fp32 -> logits [B, Cout] fp32 (a 1x1 conv on a 1x1 image + bias)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod):
+        B, Cin = x.shape
+        w = mod.weight.detach()
+        y = conv_f32(x.view(B, 1, 1, Cin), w.view(w.shape[0], 1, 1, Cin), 1, 0, 1, 1, bias=mod.bias.detach())
+        ctx.mod = mod
+        ctx.save_for_backward(x)
+        return y.view(B, -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        mod = ctx.mod
+        B, Cin = x.shape
+        Cout = dy.shape[1]
+        dy = dy.contiguous().float()
+        wt = mod.weight.detach().t().contiguous()  # [Cin][Cout]
+        dx = conv_f32(dy.view(B, 1, 1, Cout), wt.view(Cin, 1, 1, Cout), 1, 0, 1, 1).view(B, Cin)
+        wgrad_f32(dy.view(B, 1, 1, Cout), x.view(B, 1, 1, Cin), mod.weight.grad, 1, 0, 1, 1)
+        _lib.check(_k().imk_colsum_f32(dy.data_ptr(), mod.bias.grad.data_ptr(), B, Cout, _lib.stream_ptr()),
+                   "colsum f32")
+        notify_ready(mod.weight)
+        notify_ready(mod.bias)
+        return dx, None, None, None
+
+
+# ------------------------------------------------------------------ BatchNorm
+class F32Workspace:
+    """Scratch shared by every fp32 BatchNorm of a model (one stream, kernels run in order)."""
+
+    def __init__(self, device, cmax: int):
+        self.slab = torch.empty(_k().imk_bn_slab_floats_f32(cmax), device=device, dtype=torch.float32)
+        self.red = torch.empty(2 * cmax, device=device, dtype=torch.float32)
+
+
+def bn_train_f32(x: torch.Tensor, bn, ws: F32Workspace, res: Optional[torch.Tensor], relu: bool):
+    """Training BN (+ residual) (+ ReLU): batch statistics (deterministic fold), running stats
+    updated; returns (y, save [2, C] = mean, rstd)."""
+    C = x.shape[-1]
+    R = x.numel() // C
+    save = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    # the running mean is the shift of the (shifted) sums: close to the batch mean
+    _lib.check(_k().imk_bn_stats_f32(x.data_ptr(), bn.running_mean.data_ptr(), ws.slab.data_ptr(),
+                                     save.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(), R, C,
+                                     float(bn.eps), float(bn.momentum), _lib.stream_ptr()), "bn stats f32")
+    bn.num_batches_tracked.add_(1)
+    y = torch.empty_like(x)
+    _lib.check(_k().imk_bn_apply_f32(x.data_ptr(), save.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
+                                     _lib.ptr(res), y.data_ptr(), R, C, int(relu), _lib.stream_ptr()),
+               "bn apply f32")
+    return y, save
+
+
+def bn_eval_f32(x: torch.Tensor, bn, res: Optional[torch.Tensor], relu: bool) -> torch.Tensor:
+    C = x.shape[-1]
+    save = torch.stack([bn.running_mean, torch.rsqrt(bn.running_var + bn.eps)]).float().contiguous()
+    y = torch.empty_like(x)
+    _lib.check(_k().imk_bn_apply_f32(x.data_ptr(), save.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
+                                     _lib.ptr(res), y.data_ptr(), x.numel() // C, C, int(relu),
+                                     _lib.stream_ptr()), "bn eval f32")
+    return y
+
+
+class BNF32Fn(torch.autograd.Function):
+    """y = [ReLU](BN(x) [+ res]); backward: g' = g * (y > 0) -> BN backward (dgamma / dbeta into the
+    arena + reducer notification), dres = g'."""
+
+    @staticmethod
+    def forward(ctx, x, res, bn, relu, ws):
+        y, save = bn_train_f32(x, bn, ws, res, relu)
+        ctx.bn, ctx.relu, ctx.ws, ctx.has_res = bn, relu, ws, res is not None
+        ctx.save_for_backward(x, y if relu else None, save)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, save = ctx.saved_tensors
+        bn = ctx.bn
+        C = x.shape[-1]
+        R = x.numel() // C
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        _lib.check(_k().imk_bn_bwd_f32(g.data_ptr(), _lib.ptr(y), x.data_ptr(), save.data_ptr(),
+                                       bn.weight.data_ptr(), ctx.ws.slab.data_ptr(), ctx.ws.red.data_ptr(),
+                                       bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(), dx.data_ptr(),
+                                       _lib.ptr(dres), R, C, _lib.stream_ptr()), "bn bwd f32")
+        notify_ready(bn.weight)
+        notify_ready(bn.bias)
+        return dx, dres, None, None, None
+
+
+# ------------------------------------------------------------------ pooling, loss, input
+def maxpool_f32(x: torch.Tensor, k: int, s: int, p: int):
+    N, H, W, Cc = x.shape
+    OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
+    y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.float32)
+    idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
+    _lib.check(_k().imk_maxpool_f32(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, Cc, OH, OW, k, s, p,
+                                    _lib.stream_ptr()), "maxpool f32")
+    return y, idx
+
+
+class MaxPoolF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = maxpool_f32(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.cfg = (tuple(x.shape), k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        (N, H, W, Cc), k, s, p = ctx.cfg
+        OH, OW = idx.shape[1], idx.shape[2]
+        dx = torch.empty((N, H, W, Cc), device=dy.device, dtype=torch.float32)
+        _lib.check(_k().imk_maxpool_bwd_f32(dy.contiguous().data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, Cc,
+                                            OH, OW, k, s, p, _lib.stream_ptr()), "maxpool bwd f32")
+        return dx, None, None, None
+
+
+def avgpool_f32(x: torch.Tensor) -> torch.Tensor:
+    N, H, W, Cc = x.shape
+    y = torch.empty((N, Cc), device=x.device, dtype=torch.float32)
+    _lib.check(_k().imk_avgpool_f32(x.data_ptr(), y.data_ptr(), N, H * W, Cc, _lib.stream_ptr()), "avgpool f32")
+    return y
+
+
+class AvgPoolF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = tuple(x.shape)
+        return avgpool_f32(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, Cc = ctx.shape
+        dx = torch.empty(ctx.shape, device=dy.device, dtype=torch.float32)
+        _lib.check(_k().imk_avgpool_bwd_f32(dy.contiguous().data_ptr(), dx.data_ptr(), N, H * W, Cc,
+                                            _lib.stream_ptr()), "avgpool bwd f32")
+        return dx
+
+
+class XentF32Fn(torch.autograd.Function):
+    """The fused softmax-xent (+ top-k counters) of ``ops.misc.XentFn`` with an fp32 logits gradient."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, metrics, smoothing):
+        from .misc import XentFn
+        loss = XentFn.forward(ctx, logits, labels, metrics, smoothing)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, labels, lse = ctx.saved_tensors
+        B, NC = logits.shape
+        dz = torch.empty((B, NC), device=logits.device, dtype=torch.float32)
+        g = gout.to(torch.float32).contiguous()
+        _lib.check(_k().imk_xent_bwd_f32(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), g.data_ptr(),
+                                         dz.data_ptr(), B, NC, float(ctx.smoothing), _lib.stream_ptr()),
+                   "xent bwd f32")
+        return dz, None, None, None
+
+
+def normalize_u8_f32(images: torch.Tensor, out_hw, cpad: int, mean: Sequence[float], std: Sequence[float],
+                     crop: Optional[torch.Tensor] = None, flip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [B, Hs, Ws, 3] -> fp32 NHWC [B, H, W, cpad] (ToTensor + Normalize, imagenet.py:280-283)."""
+    B, Hs, Ws, _ = images.shape
+    H, W = out_hw
+    out = torch.empty((B, H, W, cpad), device=images.device, dtype=torch.float32)
+    m = (C.c_float * 3)(*mean)
+    s = (C.c_float * 3)(*std)
+    _lib.check(_k().imk_normalize_u8_f32(images.data_ptr(), out.data_ptr(), _lib.ptr(crop), _lib.ptr(flip), B, Hs,
+                                         Ws, H, W, cpad, C.cast(m, C.c_void_p), C.cast(s, C.c_void_p),
+                                         _lib.stream_ptr()), "normalize f32")
+    return out

@@ -159,7 +159,7 @@ class DataParallel(nn.Module):
             p._imagent_ready = self._mark_param
             p._imagent_index = i
         if use_autograd_hooks is None:
-            use_autograd_hooks = getattr(module, "backend", "torch") != "hip"
+            use_autograd_hooks = getattr(module, "backend", "torch") not in ("hip", "hip_f32")
         self.hooks = []
         if use_autograd_hooks:
             for p in self.arena.params:

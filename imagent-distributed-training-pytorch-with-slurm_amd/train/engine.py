@@ -73,8 +73,10 @@ class StepRunner:
             self._inflight.popleft().synchronize()
 
     def loss(self, logits, y):
-        if self.backend == "hip":
+        if self.backend in ("hip", "hip_f32"):
             from ..ops.misc import XentFn
+            if self.backend == "hip_f32":  # fp32 logits gradient
+                from ..ops.f32 import XentF32Fn as XentFn
             loss = XentFn.apply(logits, y, self.metrics.buf, self.smoothing)
             self.metrics.count_batch()
             return loss
@@ -205,6 +207,8 @@ class Trainer:
         self.kernels = a.kernels if a.kernels != "auto" else ("hip" if self.device.type == "cuda" else "torch")
         if self.kernels == "hip" and self.device.type != "cuda":
             raise RuntimeError("--kernels hip needs a GPU")
+        if self.kernels == "hip" and a.dtype == "fp32":  # the fp32 kernel path (models/native_f32.py)
+            self.kernels = "hip_f32"
         self._build_data()
         self._build_model()
         self.tb = SummaryWriter(a.tb_dir, jsonl=os.path.join(a.tb_dir, "metrics.jsonl")) \
@@ -292,7 +296,11 @@ class Trainer:
         nparams = len(list(model.parameters()))
         order = list(reversed(range(nparams)))  # backward produces grads roughly in reverse
         self.native = None
-        if self.kernels == "hip":
+        if self.kernels == "hip_f32":
+            from ..models.native_f32 import bind_native_f32
+            self.native = bind_native_f32(model, self.device, order)
+            arena = self.native.arena
+        elif self.kernels == "hip":
             from ..models.native import bind_native
             # IMAGENT_WGRAD_OVERLAP=0: weight gradients on the main stream (A/B and diagnostics)
             self.native = bind_native(model, self.device, order, fp8=a.dtype == "fp8",
