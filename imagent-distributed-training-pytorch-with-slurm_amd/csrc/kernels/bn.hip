@@ -82,19 +82,27 @@ __device__ __forceinline__ void st8(bf16_t* p, const Vec8& x) {
     *reinterpret_cast<u32x4*>(p) = w;
 }
 
+// packed 16-B row chunk: load, element i as f32, store (NT: non-temporal -- the streamed output
+// is read back by the next kernel only after far more than the L2 / MALL has passed through)
+__device__ __forceinline__ u32x4 ldw(const bf16_t* p) { return *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ float bfw(const u32x4& w, int i) { return (i & 1) ? hi_bf(w[i >> 1]) : lo_bf(w[i >> 1]); }
+template <bool NT>
+__device__ __forceinline__ void stw(bf16_t* p, const u32x4& w) {
+    if (NT) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+    else *reinterpret_cast<u32x4*>(p) = w;
+}
+
 // store the bf16 row chunk; with q: also its e5m2 copy, track |.| max in m
-__device__ __forceinline__ void st8_q(bf16_t* p, const Vec8& x, uint32_t* q, size_t off, float s, float& m) {
+template <bool NT, bool Q8>
+__device__ __forceinline__ void stq(bf16_t* p, const float (&o)[8], uint32_t* q, size_t off, float s, float& m) {
     u32x4 w;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = pack_bf2(x.v[2 * i], x.v[2 * i + 1]);
-    *reinterpret_cast<u32x4*>(p) = w;
-    if (q) {
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf2(o[2 * i], o[2 * i + 1]);
+    stw<NT>(p, w);
+    if (Q8 && q) {
         float v[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v[2 * i] = lo_bf(w[i]);
-            v[2 * i + 1] = hi_bf(w[i]);
-        }
+        for (int i = 0; i < 8; ++i) v[i] = bfw(w, i);
 #pragma unroll
         for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
         reinterpret_cast<u32x2*>(q)[off / 8] =
@@ -105,7 +113,9 @@ __device__ __forceinline__ void st8_q(bf16_t* p, const Vec8& x, uint32_t* q, siz
 
 // ---------------------------------------------------------------- forward
 // y = relu?( (x-mean)*rstd*g + b  [+ res | + (x2-mean2)*rstd2*g2 + b2] )
-template <int MODE, bool RELU>  // MODE 0: none, 1: identity residual, 2: second BN branch
+// NT: non-temporal output stores; Q8: also the e4m3 copy y8 (fp8 path; the plain kernel carries none
+// of its code: 94 -> fewer VGPRs)
+template <int MODE, bool RELU, bool NT, bool Q8>  // MODE 0: none, 1: identity residual, 2: second BN branch
 __global__ __launch_bounds__(256) void bn_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ sums, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ x2, const float* __restrict__ sums2,
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
     const int tid = threadIdx.x;
     // fp8 copy of the output for the next conv (delayed-scaled e4m3, fp8.hip)
-    const float q8 = y8 ? ldexpf(1.f, -exp8[0]) : 0.f;
+    const float q8 = Q8 ? ldexpf(1.f, -exp8[0]) : 0.f;
     float m8 = 0.f;
     if (tid >= rpb * cpr) return;  // (host: with y8, every lane is active -- C/8 divides 256)
     const int ch = tid % cpr, c0 = ch * 8;
@@ -143,42 +153,43 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     consts(sums, gamma, beta, save, sc, sh);
     if (MODE == 2) consts(sums2, gamma2, beta2, save2, sc2, sh2);
     // U rows per thread per iteration, all loads issued before any math: 4x
-    // the bytes in flight of a one-row loop (HBM needs ~72 KiB per CU)
-    const long step = (long)gridDim.x * rpb;
-    for (long r0 = (long)blockIdx.x * rpb + tid / cpr; r0 < R; r0 += U * step) {
-        Vec8 v[U], s[U];
+    // the bytes in flight of a one-row loop (HBM needs ~72 KiB per CU). The rows stay packed
+    // bf16 words until their math (unpacked early they doubled the VGPRs: 4 waves/SIMD -> 6+)
+    // block-contiguous rows: a block's iteration covers U*rpb consecutive rows (scripts/stream_bench.hip:
+    // +1-2 % over U rows gridDim*rpb apart)
+    const long step = rpb;
+    for (long r0 = (long)blockIdx.x * U * rpb + tid / cpr; r0 < R; r0 += (long)gridDim.x * U * rpb) {
+        u32x4 v[U], s[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             // unconditional loads from a clamped row: a guarded load makes hipcc branch
             // around it and wait vmcnt(0) per row (2 loads in flight instead of 2U)
             const long r = min(r0 + u * step, R - 1);
-            v[u] = ld8(x + (size_t)r * C + c0);
-            if (MODE != 0) s[u] = ld8(x2 + (size_t)r * C + c0);
+            v[u] = ldw(x + (size_t)r * C + c0);
+            if (MODE != 0) s[u] = ldw(x2 + (size_t)r * C + c0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long r = r0 + u * step;
             if (r >= R) break;
+            float o8[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                float o = fmaf(v[u].v[i], sc[i], sh[i]);
-                if (MODE == 1) o += s[u].v[i];
-                if (MODE == 2) o += fmaf(s[u].v[i], sc2[i], sh2[i]);
-                v[u].v[i] = RELU ? fmaxf(o, 0.f) : o;
+                float o = fmaf(bfw(v[u], i), sc[i], sh[i]);
+                if (MODE == 1) o += bfw(s[u], i);
+                if (MODE == 2) o += fmaf(bfw(s[u], i), sc2[i], sh2[i]);
+                o8[i] = RELU ? fmaxf(o, 0.f) : o;
             }
             u32x4 pw;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) pw[i] = pack_bf2(v[u].v[2 * i], v[u].v[2 * i + 1]);
-            *reinterpret_cast<u32x4*>(y + (size_t)r * C + c0) = pw;
-            if (y8) {
+            for (int i = 0; i < 4; ++i) pw[i] = pack_bf2(o8[2 * i], o8[2 * i + 1]);
+            stw<NT>(y + (size_t)r * C + c0, pw);
+            if (Q8) {
                 // quantise the bf16-rounded output the bf16 consumers see (unpacked
                 // from the stored words: one shift / mask per value)
                 float w[8];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    w[2 * i] = lo_bf(pw[i]);
-                    w[2 * i + 1] = hi_bf(pw[i]);
-                }
+                for (int i = 0; i < 8; ++i) w[i] = bfw(pw, i);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) m8 = fmaxf(m8, fabsf(w[i]));
                 reinterpret_cast<u32x2*>(y8)[((size_t)r * C + c0) / 8] =
@@ -187,7 +198,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
             }
         }
     }
-    if (y8) {  // every lane active (host check): block max, one atomic per block into a 32-slot amax row
+    if (Q8) {  // every lane active (host check): block max, one atomic per block into a 32-slot amax row
         __shared__ float wm[4];
         m8 = wave_max(m8);
         if ((tid & 63) == 0) wm[tid >> 6] = m8;
@@ -380,10 +391,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     }
 }
 
-// dx = gamma*rstd*(g - Sg/R - xhat*Sgx/R); MODE 1 also writes the residual
-// gradient g, MODE 2 the downsample-branch input gradient. Block 0 also adds
-// the sums into the arena slots of dgamma/dbeta (+= : gradient accumulation).
-template <int MASK, int MODE>
+// dx = gamma*rstd*(g - Sg/R - xhat*Sgx/R) = k1 g + kx x + k0 per channel; MODE 1 also writes the
+// residual gradient g, MODE 2 the downsample-branch input gradient. Block 0 also adds the sums into
+// the arena slots of dgamma/dbeta (+= : gradient accumulation). Rows stay packed bf16 words until
+// their math and the per-channel constants are three FMAs' worth (108 -> fewer VGPRs, more waves).
+template <int MASK, int MODE, bool NT, bool Q8>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -391,9 +403,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ x2, const float* __restrict__ save2, const float* __restrict__ gamma2,
     bf16_t* __restrict__ dx2, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8) {
+    constexpr int UB = MODE == 2 ? 2 : U;  // three streams in, two out: half the rows in flight
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
-    const float qs0 = g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
-    const float qs1 = g8.q[1] ? ldexpf(1.f, -g8.exp[1][0]) : 0.f;
+    const float qs0 = Q8 && g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
+    const float qs1 = Q8 && g8.q[1] ? ldexpf(1.f, -g8.exp[1][0]) : 0.f;
     float m0 = 0.f, m1 = 0.f;
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
@@ -407,62 +420,67 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
     if (tid >= rpb * cpr) return;
     const int ch = tid % cpr, c0 = ch * 8;
-    float k1[8], k2[8], k3[8], mean[8], q1[8], q2[8], q3[8], m2[8], sc[8], sh[8];
+    float k1[8], kx[8], k0[8], q1[8], qx[8], q0[8], sc[8], sh[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int c = c0 + i;
-        mean[i] = save[c];
-        const float rstd = save[C + c];
+        const float mean = save[c], rstd = save[C + c];
         const float gr = gamma[c] * rstd;
         if (MASK == 2) {
             sc[i] = gr;
-            sh[i] = beta[c] - mean[i] * gr;
+            sh[i] = beta[c] - mean * gr;
         }
         k1[i] = gr;
-        k2[i] = -gr * inv_cnt * scratch[C + c];
-        k3[i] = -gr * inv_cnt * scratch[c] * rstd;
+        kx[i] = -gr * inv_cnt * scratch[c] * rstd;
+        k0[i] = -gr * inv_cnt * scratch[C + c] - kx[i] * mean;
         if (MODE == 2) {
-            m2[i] = save2[c];
-            const float rs2 = save2[C + c];
+            const float m2 = save2[c], rs2 = save2[C + c];
             const float g2 = gamma2[c] * rs2;
             q1[i] = g2;
-            q2[i] = -g2 * inv_cnt * scratch[C + c];
-            q3[i] = -g2 * inv_cnt * scratch[2 * C + c] * rs2;
+            qx[i] = -g2 * inv_cnt * scratch[2 * C + c] * rs2;
+            q0[i] = -g2 * inv_cnt * scratch[C + c] - qx[i] * m2;
         }
     }
-    const long step = (long)gridDim.x * rpb;
-    for (long r0 = (long)blockIdx.x * rpb + tid / cpr; r0 < R; r0 += U * step) {
-        Vec8 g[U], xv[U], x2v[U];
-        u32x4 yv[U];
+    const long step = rpb;  // block-contiguous rows (see bn_fwd_kernel)
+    for (long r0 = (long)blockIdx.x * UB * rpb + tid / cpr; r0 < R; r0 += (long)gridDim.x * UB * rpb) {
+        u32x4 g[UB], xv[UB], x2v[UB], yv[UB];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UB; ++u) {
             // clamped row, unconditional loads (see bn_fwd_kernel); rows past R are not stored
             const size_t off = (size_t)min(r0 + u * step, R - 1) * C + c0;
-            g[u] = ld8(dy + off);
-            xv[u] = ld8(x + off);
-            if (MODE == 2) x2v[u] = ld8(x2 + off);
-            if (MASK == 1) yv[u] = *reinterpret_cast<const u32x4*>(y + off);
+            g[u] = ldw(dy + off);
+            xv[u] = ldw(x + off);
+            if (MODE == 2) x2v[u] = ldw(x2 + off);
+            if (MASK == 1) yv[u] = ldw(y + off);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UB; ++u) {
             const long r = r0 + u * step;
             if (r >= R) break;
             const size_t off = (size_t)r * C + c0;
-            relu_mask<MASK>(g[u], yv[u], xv[u], sc, sh);
-            Vec8 o;
+            float gv[8], o[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o.v[i] = k1[i] * g[u].v[i] + k2[i] + k3[i] * (xv[u].v[i] - mean[i]);
-            st8_q(dx + off, o, g8.q[0], off, qs0, m0);
-            if (MODE == 1) st8(dres + off, g[u]);
+            for (int i = 0; i < 8; ++i) {
+                gv[i] = bfw(g[u], i);
+                if (MASK == 1 && !(bfw(yv[u], i) > 0.f)) gv[i] = 0.f;
+                if (MASK == 2 && !(fmaf(bfw(xv[u], i), sc[i], sh[i]) > 0.f)) gv[i] = 0.f;
+                o[i] = fmaf(k1[i], gv[i], fmaf(kx[i], bfw(xv[u], i), k0[i]));
+            }
+            stq<NT, Q8>(dx + off, o, g8.q[0], off, qs0, m0);
+            if (MODE == 1) {
+                u32x4 w;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = pack_bf2(gv[2 * i], gv[2 * i + 1]);
+                stw<NT>(dres + off, w);
+            }
             if (MODE == 2) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    o.v[i] = q1[i] * g[u].v[i] + q2[i] + q3[i] * (x2v[u].v[i] - m2[i]);
-                st8_q(dx2 + off, o, g8.q[1], off, qs1, m1);
+                for (int i = 0; i < 8; ++i) o[i] = fmaf(q1[i], gv[i], fmaf(qx[i], bfw(x2v[u], i), q0[i]));
+                stq<NT, Q8>(dx2 + off, o, g8.q[1], off, qs1, m1);
             }
         }
     }
-    if (g8.q[0] || g8.q[1]) {  // every lane active (host check): block max -> slot (blockIdx & 31)
+    if (Q8) {  // every lane active (host check): block max -> slot (blockIdx & 31)
         __shared__ float wm[2][4];
         m0 = wave_max(m0);
         m1 = wave_max(m1);
@@ -475,6 +493,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             atomic_max_pos(g8.amax[tid] + (blockIdx.x & 31),
                            fmaxf(fmaxf(wm[tid][0], wm[tid][1]), fmaxf(wm[tid][2], wm[tid][3])));
     }
+}
+
+// non-temporal stores of the streamed outputs (IMAGENT_BN_NT=0 turns them off): scripts/bn_bench.py at
+// batch 1024, per step fwd 9328 -> 9077 us, bwd apply 12310 -> 12053 us
+bool bn_nt() {
+    static const bool v = [] {
+        const char* e = getenv("IMAGENT_BN_NT");
+        return !e || atoi(e) != 0;
+    }();
+    return v;
 }
 
 int grid_for(long R, int C) {
@@ -498,13 +526,20 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
     const float inv_cnt = 1.f / (float)R;
     const int grid = grid_for(R, C);
     hipStream_t st = (hipStream_t)stream;
-#define L(M, RL)                                                                                   \
-    hipLaunchKernelGGL((bn_fwd_kernel<M, RL>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
-                       gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, \
-                       R, C, inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8)
+    const bool nt = bn_nt(), q8 = y8 != nullptr;
+#define LK(M, RL, NT, Q8)                                                                               \
+    hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
+                       gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, R, C,   \
+                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8)
+#define L(M, RL)                                              \
+    do {                                                      \
+        if (q8) { if (nt) LK(M, RL, true, true); else LK(M, RL, false, true); }   \
+        else { if (nt) LK(M, RL, true, false); else LK(M, RL, false, false); } \
+    } while (0)
     if (mode == 0) { if (relu) L(0, true); else L(0, false); }
     else if (mode == 1) { if (relu) L(1, true); else L(1, false); }
     else { if (relu) L(2, true); else L(2, false); }
+#undef LK
 #undef L
     IMK_CHECK_LAUNCH();
     return 0;
@@ -549,12 +584,19 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     IMK_CHECK_LAUNCH();
     const int grid = grid_for(R, C);
     const float inv_cnt = 1.f / (float)R;
-#define LA(M)                                                                                       \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)g,   \
-                       nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr, \
-                       (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,         \
+    const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1];
+#define LK(M, NT, Q8)                                                                                \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8>), dim3(grid), dim3(256), 0, st, (const bf16_t*)g, \
+                       nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr,       \
+                       (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,               \
                        dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8)
+#define LA(M)                                                                  \
+    do {                                                                       \
+        if (q8) { if (nt) LK(M, true, true); else LK(M, false, true); }        \
+        else { if (nt) LK(M, true, false); else LK(M, false, false); }         \
+    } while (0)
     if (mode == 2) LA(2); else LA(0);
+#undef LK
 #undef LA
     IMK_CHECK_LAUNCH();
     return 0;
@@ -679,7 +721,7 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     IMK_CHECK_LAUNCH();
     const float inv_cnt = 1.f / (float)R;
 #define LA(MK, M)                                                                                  \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M, false, false>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
                        (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, folded, (bf16_t*)dx,   \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
                        dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{})

@@ -44,6 +44,17 @@ static float tail_frac() {
     return f;
 }
 
+// IMAGENT_V3_256_MINK: smallest K (= taps x C) that takes the 256x256 v3 tile (one block per CU); below
+// it the 128x128 tile (two blocks per CU) overlaps one block's epilogue with the other's main loop,
+// which is what the epilogue-heavy short-K BN-backward dgrads need (A/B: scripts/gpu_ab_v3.sh)
+static int v3_big_min_k() {
+    static const int v = [] {
+        const char* e = getenv("IMAGENT_V3_256_MINK");
+        return e ? atoi(e) : 512;  // A/B at batch 1024: 0 -> 12,782, 512 -> 12,872 img/s
+    }();
+    return v;
+}
+
 static int device_cus() {
     static const int n = [] {
         int dev = 0, cus = 0;
@@ -157,7 +168,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
-        if (a.Nout >= 512 && t8 >= 192) {
+        if (a.Nout >= 512 && t8 >= 192 && K >= v3_big_min_k()) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles
                 IGemmArgs m = a, t = a;

@@ -349,17 +349,39 @@ __global__ __launch_bounds__(256) void bn_partial_f32_kernel(const float* __rest
     }
 }
 
+// fold of the per-block partials: 64 channels per 256-thread block, 4 fixed slab partitions per
+// channel summed in double, then the 4 partition sums in order -> deterministic
+__device__ __forceinline__ void fold_slab(const float* __restrict__ slab, int nb, int C, double& a1, double& a2,
+                                          bool& active, int& c) {
+    __shared__ double red[2][4][64];
+    const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+    c = blockIdx.x * 64 + cl;
+    active = c < C;
+    double s1 = 0.0, s2 = 0.0;
+    if (active)
+        for (int b = part; b < nb; b += 4) {
+            s1 += slab[((size_t)b * 2) * C + c];
+            s2 += slab[((size_t)b * 2 + 1) * C + c];
+        }
+    red[0][part][cl] = s1;
+    red[1][part][cl] = s2;
+    __syncthreads();
+    a1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    a2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    active = active && part == 0;
+}
+
 // forward fold: save[0..C) = mean, save[C..2C) = rstd; running stats (momentum, unbiased var)
-__global__ void bn_fold_fwd_f32_kernel(const float* __restrict__ slab, int nb, const float* __restrict__ shift,
-                                       float* __restrict__ save, float* __restrict__ rmean,
-                                       float* __restrict__ rvar, long R, int C, float eps, float momentum) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double a1 = 0.0, a2 = 0.0;  // fold of the per-block fp32 partials, fixed order
-    for (int b = 0; b < nb; ++b) {
-        a1 += slab[((size_t)b * 2) * C + c];
-        a2 += slab[((size_t)b * 2 + 1) * C + c];
-    }
+__global__ __launch_bounds__(256) void bn_fold_fwd_f32_kernel(const float* __restrict__ slab, int nb,
+                                                              const float* __restrict__ shift,
+                                                              float* __restrict__ save, float* __restrict__ rmean,
+                                                              float* __restrict__ rvar, long R, int C, float eps,
+                                                              float momentum) {
+    double a1, a2;
+    bool active;
+    int c;
+    fold_slab(slab, nb, C, a1, a2, active, c);
+    if (!active) return;
     const double md = a1 / (double)R;
     const double var = fmax(a2 / (double)R - md * md, 0.0);
     const float mean = (float)(md + shift[c]);
@@ -372,15 +394,14 @@ __global__ void bn_fold_fwd_f32_kernel(const float* __restrict__ slab, int nb, c
 }
 
 // backward fold: red[0..C) = sum(g'), red[C..2C) = sum(g' xhat); dbeta / dgamma accumulate
-__global__ void bn_fold_bwd_f32_kernel(const float* __restrict__ slab, int nb, float* __restrict__ red,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int C) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double a1 = 0.0, a2 = 0.0;
-    for (int b = 0; b < nb; ++b) {
-        a1 += slab[((size_t)b * 2) * C + c];
-        a2 += slab[((size_t)b * 2 + 1) * C + c];
-    }
+__global__ __launch_bounds__(256) void bn_fold_bwd_f32_kernel(const float* __restrict__ slab, int nb,
+                                                              float* __restrict__ red, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, int C) {
+    double a1, a2;
+    bool active;
+    int c;
+    fold_slab(slab, nb, C, a1, a2, active, c);
+    if (!active) return;
     red[c] = (float)a1;
     red[C + c] = (float)a2;
     if (dbeta) dbeta[c] += (float)a1;
@@ -442,29 +463,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------ pooling, FC bias, input
-// maxpool k x k / s / p (k <= 3), NHWC, one thread per output element; idx = argmax window slot
+// maxpool k x k / s / p (k <= 3), NHWC, one thread per output pixel x 4 channels (16-B accesses);
+// idx = argmax window slot per channel
 __global__ __launch_bounds__(256) void maxpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C,
                                                           int OH, int OW, int k, int s, int p) {
-    const long total = (long)N * OH * OW * C;
+    const int C4 = C / 4;
+    const long total = (long)N * OH * OW * C4;
     for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
-        const int c = t % C;
-        const long pix = t / C;
+        const int c = (int)(t % C4) * 4;
+        const long pix = t / C4;
         const int ow = pix % OW, oh = (pix / OW) % OH, n = pix / ((long)OW * OH);
-        float best = -INFINITY;
-        int bi = 0;
+        f32x4v best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int bi[4] = {0, 0, 0, 0};
         for (int i = 0; i < k; ++i)
             for (int j = 0; j < k; ++j) {
                 const int ih = oh * s - p + i, iw = ow * s - p + j;
                 if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
-                const float v = x[(((size_t)n * H + ih) * W + iw) * C + c];
-                if (v > best || (v != v && best == best)) {
-                    best = v;
-                    bi = i * k + j;
-                }
+                const f32x4v v = *reinterpret_cast<const f32x4v*>(x + (((size_t)n * H + ih) * W + iw) * C + c);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (v[q] > best[q] || (v[q] != v[q] && best[q] == best[q])) {
+                        best[q] = v[q];
+                        bi[q] = i * k + j;
+                    }
             }
-        y[t] = best;
-        idx[t] = (uint8_t)bi;
+        *reinterpret_cast<f32x4v*>(y + pix * C + c) = best;
+        *reinterpret_cast<uint32_t*>(idx + pix * C + c) =
+            (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
     }
 }
 
@@ -473,12 +499,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_f32_kernel(const float* __res
                                                               const uint8_t* __restrict__ idx,
                                                               float* __restrict__ dx, int N, int H, int W, int C,
                                                               int OH, int OW, int k, int s, int p) {
-    const long total = (long)N * H * W * C;
+    const int C4 = C / 4;
+    const long total = (long)N * H * W * C4;
     for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
-        const int c = t % C;
-        const long pix = t / C;
+        const int c = (int)(t % C4) * 4;
+        const long pix = t / C4;
         const int iw = pix % W, ih = (pix / W) % H, n = pix / ((long)W * H);
-        float acc = 0.f;
+        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
         // windows (oh, ow) with oh*s - p <= ih <= oh*s - p + k - 1
         const int oh_lo = max(0, (ih + p - k + s) / s), oh_hi = min(OH - 1, (ih + p) / s);
         const int ow_lo = max(0, (iw + p - k + s) / s), ow_hi = min(OW - 1, (iw + p) / s);
@@ -487,9 +514,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_f32_kernel(const float* __res
                 const int i = ih - (oh * s - p), j = iw - (ow * s - p);
                 if (i < 0 || i >= k || j < 0 || j >= k) continue;
                 const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + c;
-                if (idx[o] == i * k + j) acc += dy[o];
+                const uint32_t id4 = *reinterpret_cast<const uint32_t*>(idx + o);
+                const f32x4v g = *reinterpret_cast<const f32x4v*>(dy + o);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (((id4 >> (8 * q)) & 0xff) == (uint32_t)(i * k + j)) acc[q] += g[q];
             }
-        dx[t] = acc;
+        *reinterpret_cast<f32x4v*>(dx + pix * C + c) = acc;
     }
 }
 
@@ -607,12 +638,17 @@ IMK_EXPORT int imk_bn_stats_f32(const float* x, const float* shift, float* slab,
                                 float* rvar, long R, int C, float eps, float momentum, void* stream) {
     if (C % 4 || 256 % (C / 4) || C > 1024) return -100;
     const int nb = bn_blocks(R, C);
-    hipLaunchKernelGGL((bn_partial_f32_kernel<false>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nullptr,
-                       nullptr, shift, slab, R, C);
-    IMK_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bn_fold_fwd_f32_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, slab, nb, shift,
-                       save, rmean, rvar, R, C, eps, momentum);
-    IMK_CHECK_LAUNCH();
+    // two passes: the mean (sums shifted by the caller's estimate), then the variance as the sum of
+    // squares about that mean -- no E[x^2] - E[x]^2 cancellation (PyTorch uses Welford)
+    for (int pass = 0; pass < 2; ++pass) {
+        const float* sh = pass == 0 ? shift : save;
+        hipLaunchKernelGGL((bn_partial_f32_kernel<false>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nullptr,
+                           nullptr, sh, slab, R, C);
+        IMK_CHECK_LAUNCH();
+        hipLaunchKernelGGL(bn_fold_fwd_f32_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, slab, nb,
+                           sh, save, pass ? rmean : nullptr, rvar, R, C, eps, momentum);
+        IMK_CHECK_LAUNCH();
+    }
     return 0;
 }
 
@@ -636,7 +672,7 @@ IMK_EXPORT int imk_bn_bwd_f32(const float* g, const float* y, const float* x, co
     hipLaunchKernelGGL((bn_partial_f32_kernel<true>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, g, y, save,
                        slab, R, C);
     IMK_CHECK_LAUNCH();
-    hipLaunchKernelGGL(bn_fold_bwd_f32_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, slab, nb, red,
+    hipLaunchKernelGGL(bn_fold_bwd_f32_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, slab, nb, red,
                        dgamma, dbeta, C);
     IMK_CHECK_LAUNCH();
     const long n4 = R * C / 4;
@@ -648,8 +684,8 @@ IMK_EXPORT int imk_bn_bwd_f32(const float* g, const float* y, const float* x, co
 
 IMK_EXPORT int imk_maxpool_f32(const float* x, float* y, void* idx, int N, int H, int W, int C, int OH, int OW, int k,
                                int s, int p, void* stream) {
-    if (k > 3) return -100;
-    hipLaunchKernelGGL(maxpool_f32_kernel, dim3(sgrid((long)N * OH * OW * C)), dim3(256), 0, (hipStream_t)stream, x,
+    if (k > 3 || C % 4) return -100;
+    hipLaunchKernelGGL(maxpool_f32_kernel, dim3(sgrid((long)N * OH * OW * C / 4)), dim3(256), 0, (hipStream_t)stream, x,
                        y, (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p);
     IMK_CHECK_LAUNCH();
     return 0;
@@ -657,7 +693,8 @@ IMK_EXPORT int imk_maxpool_f32(const float* x, float* y, void* idx, int N, int H
 
 IMK_EXPORT int imk_maxpool_bwd_f32(const float* dy, const void* idx, float* dx, int N, int H, int W, int C, int OH,
                                    int OW, int k, int s, int p, void* stream) {
-    hipLaunchKernelGGL(maxpool_bwd_f32_kernel, dim3(sgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream,
+    if (C % 4) return -100;
+    hipLaunchKernelGGL(maxpool_bwd_f32_kernel, dim3(sgrid((long)N * H * W * C / 4)), dim3(256), 0, (hipStream_t)stream,
                        dy, (const uint8_t*)idx, dx, N, H, W, C, OH, OW, k, s, p);
     IMK_CHECK_LAUNCH();
     return 0;

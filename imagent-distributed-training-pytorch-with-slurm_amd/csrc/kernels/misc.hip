@@ -445,12 +445,12 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__
     mx = wave_max(mx);
     float se = 0.f, sz = 0.f;
     for (int i = lane; i < NC; i += 64) {
-        se += __expf(z[i] - mx);
+        se += expf(z[i] - mx);  // precise exp/log: B x NC elements, the fp32 path's loss
         sz += z[i];
     }
     se = wave_sum(se);
     sz = wave_sum(sz);
-    const float lse = mx + __logf(se);
+    const float lse = mx + logf(se);
     const float zl = (lab >= 0 && lab < NC) ? z[lab] : 0.f;
     // rank of the label: #classes with a strictly larger logit
     int gt = 0;

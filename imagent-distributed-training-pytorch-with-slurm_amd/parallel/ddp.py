@@ -22,7 +22,9 @@ MI355X design:
 * bookkeeping (bucket plan, ready tracking, in-order launch) is the C++
   runtime (``csrc/runtime/reducer.cpp``);
 * each complete bucket is all-reduced (``ncclAvg``) on the communicator's
-  high-priority side stream, ordered after the producing kernels by an event;
+  own comm stream (normal priority: a high-priority one measured -15 %,
+  profiles/r50_b1024_comm_stream_study.md), ordered after the producing
+  kernels by an event;
   the compute stream joins once at the end of backward. Bucket sizes target
   xGMI: a small first bucket (fc grads are ready first) and mid-size caps
   so several collectives overlap the remaining backward.

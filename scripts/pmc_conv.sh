@@ -17,4 +17,4 @@ run SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_AN
 run SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
 run FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE
 cd $R
-for p in $D/*/; do python3 scripts/pmc_kernels.py $(ls $p/*.db | head -1) --grep igemm; done > $D/summary.txt
+for p in $D/*/; do python3 scripts/pmc_kernels.py $(ls $p/*.db | head -1) ; done > $D/summary.txt

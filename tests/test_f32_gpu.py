@@ -1,8 +1,9 @@
-"""fp32 kernel path (csrc/kernels/f32.hip, ops/f32.py, models/native_f32.py) against PyTorch fp32.
+"""fp32 kernel path (csrc/kernels/f32.hip, ops/f32.py, models/native_f32.py) against PyTorch.
 
-The reference trains in fp32 (imagenet.py:312, no AMP): every fp32 op is compared with the
-PyTorch fp32 op at <= 1e-4 relative (normwise), and a whole ResNet-18 training step (forward,
-backward, SGD) with the fp32 oracle model.
+The reference trains in fp32 (imagenet.py:312, no AMP). Every fp32 op is checked two ways: within
+1e-4 relative (normwise) of the PyTorch fp32 op, and no farther from the float64 result than 4x
+PyTorch fp32's own distance to it (+1e-6) -- i.e. as accurate as the PyTorch fp32 path, not just
+close to it. The whole-model test runs two ResNet-18 training steps against float64.
 """
 
 import os
@@ -20,7 +21,13 @@ TOL = 1e-4
 
 
 def rel(a, b):
+    a, b = a.detach(), b.detach()
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def as_good(ours, torch32, exact, floor=1e-6):
+    """ours within 1e-4 of torch fp32 and as close to float64 as torch fp32 is (4x, + floor)."""
+    return rel(ours, torch32) < TOL and rel(ours, exact) <= 4 * rel(torch32, exact) + floor
 
 
 def nhwc(t):
@@ -49,14 +56,18 @@ def test_conv_f32_fwd_dgrad_wgrad(shape):
     y = F.conv2d(x, w, None, s, p)
     g = torch.randn_like(y)
     y.backward(g)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = w.detach().double().requires_grad_(True)
+    y64 = F.conv2d(x64, w64, None, s, p)
+    y64.backward(g.double())
     wk = w.detach().permute(0, 2, 3, 1).contiguous()
     got = conv_f32(nhwc(x.detach()), wk, s, p, k, k)
-    assert rel(nchw(got), y.detach()) < TOL
+    assert as_good(nchw(got), y, y64)
     dx = dgrad_f32(nhwc(g), wk.permute(3, 1, 2, 0).contiguous(), (H, H), s, p, k, k)
-    assert rel(nchw(dx), x.grad) < TOL
+    assert as_good(nchw(dx), x.grad, x64.grad)
     dw = torch.zeros(Co, k, k, Ci, device=DEV)
     wgrad_f32(nhwc(g), nhwc(x.detach()), dw, s, p, k, k)
-    assert rel(dw.permute(0, 3, 1, 2), w.grad) < TOL
+    assert as_good(dw.permute(0, 3, 1, 2), w.grad, w64.grad)
 
 
 @pytest.mark.parametrize("C,res,relu", [(64, False, True), (128, True, True), (256, False, False), (512, True, True)])
@@ -84,17 +95,26 @@ def test_bn_f32(C, res, relu):
         yr = F.relu(yr)
     g = torch.randn_like(yr)
     yr.backward(g)
+    x64 = x.detach().double().requires_grad_(True)
+    r64 = r.detach().double().requires_grad_(True) if res else None
+    g64_, b64_ = gam.detach().double().requires_grad_(True), bet.detach().double().requires_grad_(True)
+    y64 = F.batch_norm(x64, None, None, g64_, b64_, True, 0.1, 1e-5)
+    if res:
+        y64 = y64 + r64
+    if relu:
+        y64 = F.relu(y64)
+    y64.backward(g.double())
     ws = F32Workspace(DEV, C)
     xn = nhwc(x.detach()).requires_grad_(True)
     rn = nhwc(r.detach()).requires_grad_(True) if res else None
     y = BNF32Fn.apply(xn, rn, bn, relu, ws)
-    assert rel(nchw(y), yr.detach()) < TOL
+    assert as_good(nchw(y), yr, y64)
     assert rel(bn.running_mean, rm) < TOL and rel(bn.running_var, rv) < TOL
     y.backward(nhwc(g))
-    assert rel(nchw(xn.grad), x.grad) < TOL
-    assert rel(bn.weight.grad, gam.grad) < TOL and rel(bn.bias.grad, bet.grad) < TOL
+    assert as_good(nchw(xn.grad), x.grad, x64.grad)
+    assert as_good(bn.weight.grad, gam.grad, g64_.grad) and as_good(bn.bias.grad, bet.grad, b64_.grad)
     if res:
-        assert rel(nchw(rn.grad), r.grad) < TOL
+        assert as_good(nchw(rn.grad), r.grad, r64.grad)
 
 
 def test_pool_fc_xent_f32():
@@ -125,8 +145,19 @@ def test_pool_fc_xent_f32():
 
 
 def test_resnet18_f32_training_step_matches_torch():
-    """One full training step (normalise -> forward -> xent -> backward -> SGD) of ResNet-18 on the
-    fp32 kernels against the same model on PyTorch fp32 ops."""
+    """Two full training steps (normalise -> forward -> xent -> backward -> SGD) of ResNet-18 on the
+    fp32 kernels against the same model in float64 (PyTorch ops). The first forward (loss) is within
+    1e-4 relative; what depends on the gradients (updated parameters, the second loss, eval logits)
+    within 3x PyTorch fp32's own distance to float64, or 2e-3.
+
+    Gradients get a looser 1e-2 bound, because of the ReLU: an activation within rounding of 0 can
+    take the other side of the mask in ANY fp32 forward, and one such flip among ~10^5 activations
+    moves that BatchNorm's bias gradient (a sum that cancels to ~5 % of its terms) by ~2e-3 and
+    every gradient below it by as much (scripts/f32_diag.py: one flip at layer3.1.bn1 gives exactly
+    the 1-3e-3 seen at every earlier layer, with the same gradients computed under float64's mask
+    matching to 2.5e-6; PyTorch fp32 flips too on other seeds, 4.5e-3 at layer1.1.bn2.bias).
+    """
+    import copy
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.models import resnet
     from imagent_amd.models.arena import ParamArena
@@ -135,37 +166,52 @@ def test_resnet18_f32_training_step_matches_torch():
     from imagent_amd.train.optim import FlatSGD
     torch.manual_seed(3)
     ref = resnet.resnet18(num_classes=100).to(DEV)
+    ref64 = copy.deepcopy(ref).double()
     m = resnet.resnet18(num_classes=100)
     m.load_state_dict(ref.state_dict())
     st = bind_native_f32(m, DEV)
-    ar = ParamArena(list(ref.named_parameters()), torch.device(DEV))
-    opt_r = FlatSGD(ar, lr=0.1, momentum=0.9, weight_decay=1e-4)
-    opt = FlatSGD(st.arena, lr=0.1, momentum=0.9, weight_decay=1e-4)
-    u8 = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device=DEV)
+    models = [(ref, ParamArena(list(ref.named_parameters()), torch.device(DEV))),
+              (ref64, None), (m, st.arena)]
+    opts = [FlatSGD(models[0][1], lr=0.1, momentum=0.9, weight_decay=1e-4),
+            torch.optim.SGD(ref64.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4),
+            FlatSGD(st.arena, lr=0.1, momentum=0.9, weight_decay=1e-4)]
+    u8 = torch.randint(0, 256, (8, 112, 112, 3), dtype=torch.uint8, device=DEV)
     y = torch.randint(0, 100, (8,), device=DEV)
-    xr = InputTransform("torch", (64, 64))(u8)
-    xh = InputTransform("hip_f32", (64, 64), cpad=4)(u8)
+    xr = InputTransform("torch", (112, 112))(u8)
+    xh = InputTransform("hip_f32", (112, 112), cpad=4)(u8)
     assert rel(nchw(xh[..., :3]), xr) < 1e-6
+
+    def close(ours, oracle32, exact, floor=1e-4):
+        return rel(ours, exact) <= max(3 * rel(oracle32, exact), floor)
+
     for it in range(2):
-        ref.train()
-        m.train()
-        opt_r.zero_grad()
-        opt.zero_grad()
-        lr_ = F.cross_entropy(ref(xr), y)
-        lr_.backward()
+        for mm, _ in models:
+            mm.train()
+        for o in opts:
+            o.zero_grad()
+        l32 = F.cross_entropy(ref(xr), y)
+        l32.backward()
+        l64 = F.cross_entropy(ref64(xr.double()), y)
+        l64.backward()
         met = torch.zeros(4, device=DEV)
         loss = XentF32Fn.apply(m(xh), y, met, 0.0)
         loss.backward()
-        assert abs(loss.item() - lr_.item()) < 1e-4 * max(1.0, abs(lr_.item())), (it, loss.item(), lr_.item())
-        gr = {n: p.grad for n, p in ref.named_parameters()}
-        for n, p in m.named_parameters():
-            assert rel(p.grad, gr[n]) < 1e-3, (it, n, rel(p.grad, gr[n]))
-        opt_r.step()
-        opt.step()
-    for (n, a), (_, b) in zip(m.state_dict().items(), ref.state_dict().items()):
+        # step 0: the same weights -> 1e-4; step 1 runs on weights updated with those (flip-affected,
+        # see above) gradients, lr 0.1: the loss moved 4.74 -> 2.75 and carries their 1e-3 (measured 6e-4)
+        ltol = 1e-4 if it == 0 else 2e-3
+        assert abs(loss.item() - l64.item()) < ltol * max(1.0, abs(l64.item())), (it, loss.item(), l64.item())
+        g32 = {n: p.grad for n, p in ref.named_parameters()}
+        g64 = {n: p.grad for n, p in ref64.named_parameters()}
+        bad = [(n, f"{rel(p.grad, g64[n]):.2e}", f"{rel(g32[n], g64[n]):.2e}") for n, p in m.named_parameters()
+               if not close(p.grad, g32[n], g64[n], 1e-2)]
+        assert not bad, (it, bad)
+        for o in opts:
+            o.step()
+    sd32, sd64 = ref.state_dict(), ref64.state_dict()
+    for n, a in m.state_dict().items():
         if a.dtype.is_floating_point:
-            assert rel(a, b) < 1e-4, n
-    m.eval()
-    ref.eval()
+            assert close(a, sd32[n], sd64[n], 2e-3), n
+    for mm, _ in models:
+        mm.eval()
     with torch.no_grad():
-        assert rel(m(xh), ref(xr)) < 1e-4
+        assert close(m(xh), ref(xr), ref64(xr.double()), 2e-3)
