@@ -429,14 +429,17 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
-    // K = 256 / 512 into > 128 channels (bottleneck conv3 / downsample forwards): 64-channel
+    // K = 256 into > 128 channels (bottleneck conv3 / downsample forwards): 64-channel
     // weight slices resident in LDS, the slices of one pixel range on one XCD (the pixels
     // are fetched from HBM once and re-read from that XCD's L2). IMAGENT_STREAM_WIDE=0: tiles.
-    static const bool wide = [] {
+    // Only K = 256: at K = 512 the v3 tiles win (conv_bench at 1024 img: 512 -> 2048 @7 fwd 210 -> 179 us,
+    // 512 -> 1024 /2 @28 443 -> 375, 2048 -> 512 dgrad 209 -> 152; K = 256 stays here: 256 -> 1024 @14
+    // fwd 264 vs 370). IMAGENT_STREAM_WIDE=2: K = 512 too.
+    static const int wide = [] {
         const char* e = getenv("IMAGENT_STREAM_WIDE");
-        return !e || e[0] != '0';
+        return e ? atoi(e) : 1;
     }();
-    if (wide && !(a.flags & IG_BNBWD) && (a.C == 256 || a.C == 512) && a.Nout > 128) {
+    if (wide && !(a.flags & IG_BNBWD) && (a.C == 256 || (a.C == 512 && wide == 2)) && a.Nout > 128) {
         if (bn != 0 && bn != 64) return 1;
         return a.C == 256 ? launch_stream1<256, 64, 2, 0>(a, st) : launch_stream1<512, 64, 1, 0>(a, st);
     }
