@@ -281,6 +281,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
         }
 }
 
+}  // namespace
+
+#include "conv_wgrad_v3.h"
+
+namespace {
+
 int xf_target() {  // IMAGENT_WGRAD_XF_TARGET: blocks of a folded-BN wgrad (0: the generic target)
     static const int t = [] {
         const char* e = getenv("IMAGENT_WGRAD_XF_TARGET");
@@ -361,12 +367,49 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
         return launch<64, 128, 1, true>(a, splits, st);
     }
     if (a.Ci % 8 || a.Co % 8) return -100;
+    // LDS-DMA main loop (conv_wgrad_v3.h) for the 1x1 convs it covers (conv_bench at 1024 img: 1x1
+    // wgrads -790 us per step in total, e.g. 512 -> 256 @28 457 -> 325 us; on 3x3 the register-staged
+    // kernel stays ahead, 128 @28 452 vs 497). IMAGENT_WGRAD_V3 = 0 off, 1 (default) 1x1 with 64-row
+    // stages x 2, 2: 64 x 3, 3: 32 x 4, 4: 128 x 2, 5: 64 x 2 for every shape it covers
+    static const int v3 = [] {
+        const char* e = getenv("IMAGENT_WGRAD_V3");
+        return e ? atoi(e) : 1;
+    }();
+    if (v3 && wgrad_v3_ok(a) && (v3 == 5 || (a.KH == 1 && a.KW == 1))) {
+        switch (v3) {
+            case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
+            case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
+            case 4: return launch_wgrad_v3<128, 2>(a, splits, st);
+            default: return launch_wgrad_v3<64, 2>(a, splits, st);
+        }
+    }
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
     // 2 % slower than this register-staged loop on every R50 shape: not kept)
     // (launch<256, 256, 2, false, 8> -- one 8-wave block per CU -- measured 23 %
     // slower in total: this register-staged loop needs two blocks per CU)
     return launch<128, 128, 2, false>(a, splits, st);
+}
+
+// explicit kernel choice (tests, A/B): -1 the register-staged kernel, 1..4 the v3 variants of
+// IMAGENT_WGRAD_V3 (-106 when the shape is not one v3 covers), 0 the default dispatch
+IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int variant, void* stream) {
+    const WgradArgs& a = *args;
+    if (variant == 0) return imk_conv_wgrad(args, splits, stream);
+    if (a.M <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (variant < 0) {
+        if (a.stem || a.dYx || a.xbn || a.Ci % 8 || a.Co % 8) return -106;
+        return a.Co <= 64 ? launch<64, 128, 1, false>(a, splits, st) : launch<128, 128, 2, false>(a, splits, st);
+    }
+    if (!wgrad_v3_ok(a)) return -106;
+    switch (variant) {
+        case 1: return launch_wgrad_v3<64, 2>(a, splits, st);
+        case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
+        case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
+        case 4: return launch_wgrad_v3<128, 2>(a, splits, st);
+        default: return -106;
+    }
 }
 
 IMK_EXPORT int imk_wgrad_args_size() { return (int)sizeof(WgradArgs); }

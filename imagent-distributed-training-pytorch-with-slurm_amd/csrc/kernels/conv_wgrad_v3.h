@@ -1,0 +1,220 @@
+// Weight-gradient main loop v3 for gfx950 (MI355X): dW[co][tap*Ci + ci] += sum_m dY[m][co] X[g(m,tap)][ci]
+// for Ci % 128 == 0 and Co % 128 == 0 (every R50 3x3 but 64 -> 64, the K >= 128 1x1 convs) -- cuDNN's
+// conv wgrad inside loss.backward() in the reference (/root/reference/imagenet.py:128).
+//
+// Why a second kernel: the register-staged wgrad_kernel (conv_wgrad.hip) measured 21.5 % MFMA busy
+// on 128@28 3x3 with 6.4 VALU instructions per MFMA (scripts/pmc_conv.sh): every operand chunk goes
+// global -> VGPR -> LDS with a 64-bit address and, for X, two magic-number divisions per row and
+// stage. Here both operands are LDS-DMA fills through BUFFER descriptors (as igemm_v3_kernel):
+//  * dY rows are contiguous in m: the lane offset is fixed, the stage advance is one add, rows past
+//    M fall outside the descriptor's range (zeros);
+//  * a k-tile is ONE filter tap x 128 input channels (Ci % 128 == 0), so every X row of a stage
+//    has the same tap shift: one gather (img, ih, iw) per row and stage, out-of-image taps as an
+//    out-of-range offset (zeros) -- no zero line, no per-chunk address math;
+//  * LDS image: plain 256-B rows, chunk ch of row r at slot ch ^ (((r&3)<<2) | ((r>>2)&3))
+//    (cdna_hip_programming.md T10 image (b)); the DMA lane -> (row, chunk) map applies the XOR on
+//    the source side, so a 1-KB DMA instruction fills 4 whole rows;
+//  * fragments by the transposing LDS read ds_read_b64_tr_b16 (rows = pixels = MFMA k); a 32-lane
+//    half reads two 4-row blocks 8 rows apart (conflict-free on image (b)); the pixel order inside a
+//    fragment is permuted identically for both operands (the sum over m does not care);
+//  * NS-deep ring, counted vmcnt + one s_barrier per stage, split-K over m with fp32 atomics into
+//    the gradient arena (as wgrad_kernel), XCD-aware block order: the tiles of one m-range share
+//    an XCD (and its L2).
+
+#pragma once
+
+#include "common.h"
+
+namespace {
+
+constexpr uint32_t WG3_OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wg3_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void wg3_dma(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ int wg3_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// BR: pixel rows per stage (multiple of 32); NS: ring depth. 4 waves, 2 x 2 over a 128 x 128 tile.
+template <int BR, int NS>
+__global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
+    constexpr int SB = BR * 256;          // bytes per operand per stage
+    constexpr int PPW = BR / 16;          // 1-KB pieces per wave per operand per stage
+    constexpr int LPS = 2 * PPW;          // DMA instructions per wave per stage
+    constexpr int NKS = BR / 32;          // MFMA k-steps per stage
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sD = smem;
+    char* sX = smem + NS * SB;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wco = wid & 1, wkc = wid >> 1;
+    const int K = a.KH * a.KW * a.Ci;
+    const int nco = a.Co / 128, nkc = K / 128;
+    const int ntiles = nco * nkc;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = lid % ntiles, split = lid / ntiles;
+    const int co0 = (tile % nco) * 128, kc0 = (tile / nco) * 128;
+    const int mbeg = split * a.m_per_split;
+    if (mbeg >= a.M) return;
+    const int mend = min(a.M, mbeg + a.m_per_split);
+    const int nst = (mend - mbeg + BR - 1) / BR;
+    const int tap = kc0 / a.Ci, ci0 = kc0 - tap * a.Ci;
+    const int dh = tap / a.KW - a.pad, dw = tap % a.KW - a.pad;
+
+    // descriptors: the column offset (co0 / ci0) in the base, so a row's offset is row * ld * 2 +
+    // chunk * 16 and anything at or past row M (dY) is out of range
+    const __amdgpu_buffer_rsrc_t rd = wg3_rsrc(a.dY + co0, (uint32_t)((size_t)a.M * a.Co * 2 - co0 * 2));
+    const __amdgpu_buffer_rsrc_t rx =
+        wg3_rsrc(a.X + ci0, (uint32_t)((size_t)a.N * a.H * a.W * a.Ci * 2 - ci0 * 2));
+
+    // this lane's DMA slot: row (within the 4-row piece) and source chunk
+    const int prow = lane >> 4;
+    const int ohw = a.OH * a.OW;
+    const bool dense = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.OH == a.H && a.OW == a.W;
+    uint32_t voffd[PPW], rowcs[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        const int r = (wid * PPW + q) * 4 + prow;  // row within the stage
+        const int ch = (lane & 15) ^ wg3_swz(r);
+        rowcs[q] = (uint32_t)(ch * 16);
+        voffd[q] = (uint32_t)((mbeg + r) * a.Co * 2) + rowcs[q];
+    }
+    const uint32_t dstep = (uint32_t)(BR * a.Co * 2);
+
+    int is = 0;
+    auto issue = [&]() {
+        if (is >= nst) return;
+        const int buf = is % NS;
+        char* dD = sD + buf * SB + wid * PPW * 1024;
+        char* dX = sX + buf * SB + wid * PPW * 1024;
+        const int mb = mbeg + is * BR;
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) wg3_dma(rd, dD + q * 1024, voffd[q] + (uint32_t)is * dstep);
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) {
+            const int m = mb + (wid * PPW + q) * 4 + prow;
+            uint32_t off = WG3_OOB;
+            if (dense) {
+                if (m < mend) off = (uint32_t)m * (uint32_t)(a.Ci * 2) + rowcs[q];
+            } else if (m < mend) {
+                const uint32_t img = fdiv((uint32_t)m, a.mg_ohw, a.sh_ohw);
+                const uint32_t rem = (uint32_t)m - img * (uint32_t)ohw;
+                const uint32_t oh = fdiv(rem, a.mg_ow, a.sh_ow);
+                const uint32_t ow = rem - oh * (uint32_t)a.OW;
+                const int ih = (int)oh * a.stride + dh, iw = (int)ow * a.stride + dw;
+                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                    off = ((img * (uint32_t)a.H + (uint32_t)ih) * (uint32_t)a.W + (uint32_t)iw) * (uint32_t)(a.Ci * 2) +
+                          rowcs[q];
+            }
+            wg3_dma(rx, dX + q * 1024, off);
+        }
+        ++is;
+    };
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue();
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // transposed-read addressing: group g = lane >> 4 reads rows R1 + q and R1 + 16 + q
+    // (R1 = (g & 1) * 8 + (g >> 1) * 4: a 32-lane half's two blocks 8 rows apart), columns
+    // c0 + 4p .. +3 of chunk (c0 / 8 + (p >> 1)) ^ swz(row), byte 8 * (p & 1)
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int r1 = (g & 1) * 8 + (g >> 1) * 4 + q4, r2 = r1 + 16;
+    int offa[4][2], offb[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int ca = wco * 8 + 2 * i + (p4 >> 1), cb = wkc * 8 + 2 * i + (p4 >> 1);
+        offa[i][0] = r1 * 256 + ((ca ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
+        offa[i][1] = r2 * 256 + ((ca ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
+        offb[i][0] = r1 * 256 + ((cb ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
+        offb[i][1] = r2 * 256 + ((cb ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
+    }
+
+    for (int s = 0; s < nst; ++s) {
+        if (is - 1 - s >= NS - 2)
+            __builtin_amdgcn_s_waitcnt((((NS - 2) * LPS) & 0xF) | ((((NS - 2) * LPS) >> 4) << 14) | (0x7 << 4) |
+                                       (0xF << 8));
+        else
+            __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        __builtin_amdgcn_s_barrier();
+        issue();
+        const int buf = s % NS;
+        const char* bD = sD + buf * SB;
+        const char* bX = sX + buf * SB;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            bf16x8 fd[4], fx[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(bD + ks * 8192 + offa[i][0]));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(bD + ks * 8192 + offa[i][1]));
+                fd[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(bX + ks * 8192 + offb[j][0]));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(bX + ks * 8192 + offb[j][1]));
+                fx[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[i], fx[j], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // acc[i][j][r]: co = co0 + wco*64 + i*16 + (lane>>4)*4 + r ; k = kc0 + wkc*64 + j*16 + (lane&15)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float* dst = a.dW + (size_t)(co0 + wco * 64 + i * 16 + (lane >> 4) * 4 + r) * K + kc0 + wkc * 64 + (lane & 15);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) atomicAdd(dst + j * 16, acc[i][j][r]);
+        }
+}
+
+// shapes this kernel covers (host): one tap per 128-wide k tile, whole 128-channel co tiles,
+// byte offsets of both operands below 2^31
+bool wgrad_v3_ok(const WgradArgs& a) {
+    if (a.stem || a.dYx || a.xbn || a.Ci % 128 || a.Co % 128) return false;
+    if ((size_t)a.M * a.Co * 2 >= (1u << 31) || (size_t)a.N * a.H * a.W * a.Ci * 2 >= (1u << 31)) return false;
+    return true;
+}
+
+template <int BR, int NS>
+int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
+    const int K = a.KH * a.KW * a.Ci;
+    const int ntiles = (a.Co / 128) * (K / 128);
+    if (splits <= 0) {
+        static const int tgt_env = [] {
+            const char* e = getenv("IMAGENT_WGRAD_TARGET");
+            return e ? atoi(e) : 0;
+        }();
+        const int target = tgt_env > 0 ? tgt_env : 1024;  // ~4 blocks per CU over 256 CUs
+        const int want = (target + ntiles - 1) / ntiles;
+        const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
+        splits = max(1, min(want, maxs));
+    }
+    int mps = (a.M + splits - 1) / splits;
+    mps = (mps + BR - 1) / BR * BR;  // whole stages: a split's last stage never reads the next split's rows
+    splits = (a.M + mps - 1) / mps;
+    a.m_per_split = mps;
+    const size_t lds = (size_t)NS * 2 * BR * 256;
+    hipLaunchKernelGGL((wgrad_v3_kernel<BR, NS>), dim3(ntiles * splits), dim3(256), lds, st, a);
+    CONV_COUNTED();
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace

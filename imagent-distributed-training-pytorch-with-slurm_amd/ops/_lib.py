@@ -135,6 +135,7 @@ def _declare(name: str, lib) -> None:
         sigs = {
             "imk_conv_igemm": [C.POINTER(IGemmArgs), i32, vp],
             "imk_conv_wgrad": [C.POINTER(WgradArgs), i32, vp],
+            "imk_conv_wgrad_variant": [C.POINTER(WgradArgs), i32, i32, vp],
             "imk_conv_launches": [],
             # fp32 path (f32.hip)
             "imk_conv_f32": [C.POINTER(IGemmArgs), vp],

@@ -270,10 +270,13 @@ class BNBwdFuse:
 
 
 def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int, KH: int,
-                KW: int, splits: int = 0, stem: bool = False, xbn: Optional[torch.Tensor] = None) -> None:
+                KW: int, splits: int = 0, stem: bool = False, xbn: Optional[torch.Tensor] = None,
+                variant: int = 0) -> None:
     """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci]).
     ``stem``: x has 4 channels, dw is ``[Co][KH][32]`` (see :func:`igemm_fwd`).
-    ``xbn``: the X operand is relu(x * xbn[0] + xbn[1]) (1x1 convs; as in :func:`igemm_fwd`)."""
+    ``xbn``: the X operand is relu(x * xbn[0] + xbn[1]) (1x1 convs; as in :func:`igemm_fwd`).
+    ``variant`` (tests / A/B): 0 the default dispatch, -1 the register-staged kernel, 1..4 the
+    LDS-DMA v3 kernel's stage shapes (conv_wgrad_v3.h)."""
     N, H, W, Ci = x.shape
     _, OH, OW, Co = dy.shape
     if stem:
@@ -290,6 +293,10 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     if xbn is not None:
         assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
         a.xbn = xbn.data_ptr()
+    if variant:
+        _lib.check(_lib.kernels().imk_conv_wgrad_variant(C.byref(a), splits, variant, _lib.stream_ptr()),
+                   f"conv wgrad variant {variant}")
+        return
     _wgrad_call(a, splits, _lib.stream_ptr(), "conv wgrad")
 
 

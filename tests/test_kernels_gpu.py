@@ -189,6 +189,27 @@ def test_wgrad_variants(shape, splits):
     assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3
 
 
+@pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4])
+@pytest.mark.parametrize("shape", [(4, 128, 14, 128, 3, 1, 1), (3, 256, 9, 128, 3, 2, 1), (2, 128, 7, 256, 3, 1, 1),
+                                   (3, 256, 11, 384, 1, 1, 0), (2, 128, 10, 256, 1, 2, 0), (1, 128, 5, 128, 3, 1, 1)])
+def test_wgrad_v3(shape, variant):
+    """LDS-DMA weight gradient (conv_wgrad_v3.h, Ci % 128 == 0, Co % 128 == 0) and the register-staged
+    kernel on the same shapes: 3x3 stride 1 / 2 with image borders, 1x1 dense and strided, an M that
+    is not a multiple of the stage rows, explicit split-K."""
+    from imagent_amd.ops.conv import igemm_wgrad
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(7)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = torch.randn(Co, Ci, k, k, device=DEV).requires_grad_(True)
+    yr = F.conv2d(x.float(), w, None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    for splits in (0, 3):
+        dw = torch.zeros(Co, k, k, Ci, device=DEV)
+        igemm_wgrad(nhwc(g), nhwc(x), dw, s, p, k, k, splits=splits, variant=variant)
+        assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
+
+
 def test_stem_row_segment_conv():
     """7x7/s2 stem: 4-channel NHWC input, [Co][KH][32] weight rows (fwd + wgrad)."""
     from imagent_amd.ops.conv import igemm_fwd, igemm_wgrad
