@@ -121,7 +121,8 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     const float* __restrict__ beta, const bf16_t* __restrict__ x2, const float* __restrict__ sums2,
     const float* __restrict__ gamma2, const float* __restrict__ beta2, bf16_t* __restrict__ y,
     float* __restrict__ save, float* __restrict__ save2, long R, int C, float inv_cnt, float eps,
-    int eval, uint32_t* __restrict__ y8, const int* __restrict__ exp8, float* __restrict__ amax8) {
+    int eval, uint32_t* __restrict__ y8, const int* __restrict__ exp8, float* __restrict__ amax8,
+    uint8_t* __restrict__ ym) {
     const int cpr = C / 8;                // chunks per row
     const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
     const int tid = threadIdx.x;
@@ -184,6 +185,15 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) pw[i] = pack_bf2(o8[2 * i], o8[2 * i + 1]);
             stw<NT>(y + (size_t)r * C + c0, pw);
+            if (MODE != 0 && RELU && ym) {  // the ReLU mask as bits for the backward's dgrad epilogue
+                uint32_t b = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {  // stored bf16 > 0: nonzero, sign clear, not NaN
+                    const uint32_t h = (pw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                    b |= (h != 0u && h <= 0x7F80u ? 1u : 0u) << i;
+                }
+                ym[((size_t)r * C + c0) >> 3] = (uint8_t)b;
+            }
             if (Q8) {
                 // quantise the bf16-rounded output the bf16 consumers see (unpacked
                 // from the stored words: one shift / mask per value)
@@ -516,11 +526,13 @@ int grid_for(long R, int C) {
 
 // mode: 0 plain, 1 + identity residual (x2), 2 + second BN branch (x2, sums2, gamma2, beta2)
 // y8 (optional): e4m3 copy of y quantised with 2^-exp8[0]; amax8 ([32] slots,
-// folded by imk_fp8_update_exp) receives max |y|
+// folded by imk_fp8_update_exp) receives max |y|; ym (optional, modes 1 / 2 with ReLU): the mask
+// y > 0 as bits, byte e/8 of element e (IGemmArgs.bnym)
 IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, const float* beta,
                           const void* x2, const float* sums2, const float* gamma2, const float* beta2,
                           void* y, float* save, float* save2, long R, int C, int mode, int relu,
-                          float eps, int eval, void* y8, const int* exp8, float* amax8, void* stream) {
+                          float eps, int eval, void* y8, const int* exp8, float* amax8, void* ym,
+                          void* stream) {
     if (C % 8 || C > 2048) return -100;
     if (y8 && (256 % (C / 8) || !exp8 || !amax8)) return -102;
     const float inv_cnt = 1.f / (float)R;
@@ -530,7 +542,7 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
 #define LK(M, RL, NT, Q8)                                                                               \
     hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
                        gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, R, C,   \
-                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8)
+                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym)
 #define L(M, RL)                                              \
     do {                                                      \
         if (q8) { if (nt) LK(M, RL, true, true); else LK(M, RL, false, true); }   \

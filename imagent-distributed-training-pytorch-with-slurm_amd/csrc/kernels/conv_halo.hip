@@ -156,7 +156,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
     const int ec = lane & 7, ep0 = 32 * wid + (lane >> 3);
     const bool want_st = a.stats != nullptr;
     const bool accum = a.flags & IG_ACCUM;
-    const bool has_y = EPI == 1 && a.bny != nullptr, has_x2 = EPI == 1 && a.bnx2 != nullptr;
+    const bool has_y = EPI == 1 && a.bnym != nullptr, has_x2 = EPI == 1 && a.bnx2 != nullptr;
     float c0[8], c1[8], c2[8], c3[8];  // per-channel constants (see below)
     float s1[8], s2[8], s3[8];
 #pragma unroll
@@ -245,11 +245,12 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
             float v[8];
             unpack8(*reinterpret_cast<const u32x4*>(sE + p * HALO_SP + ec * 16), v);
             bf16_t* yp = reinterpret_cast<bf16_t*>(a.Y) + e;
-            u32x4 xw = {0u, 0u, 0u, 0u}, yw = xw, x2w = xw, ow = xw;
+            u32x4 xw = {0u, 0u, 0u, 0u}, x2w = xw, ow = xw;
+            uint32_t yw = 0u;
             if (accum) ow = *reinterpret_cast<const u32x4*>(yp);
             if (EPI == 1) {
                 xw = *reinterpret_cast<const u32x4*>(a.bnx + e);
-                if (has_y) yw = *reinterpret_cast<const u32x4*>(a.bny + e);
+                if (has_y) yw = a.bnym[e >> 3];
                 if (has_x2) x2w = *reinterpret_cast<const u32x4*>(a.bnx2 + e);
             }
             if (accum) {
@@ -262,7 +263,8 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                 float xv[8], mk[8];
                 unpack8(xw, xv);
                 if (has_y) {
-                    unpack8(yw, mk);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) mk[q] = (yw >> q) & 1u ? 1.f : 0.f;
                 } else {
 #pragma unroll
                     for (int q = 0; q < 8; ++q) mk[q] = fmaf(xv[q], c2[q], c3[q]);
@@ -377,7 +379,7 @@ int conv_halo(const IGemmArgs& a, hipStream_t st) {
     if (a.kh0 + 2 * a.khs < 0 || a.kh0 + 2 * a.khs > 2 || a.kh0 < 0 || a.kh0 > 2) return 1;
     if (a.kw0 + 2 * a.kws < 0 || a.kw0 + 2 * a.kws > 2 || a.kw0 < 0 || a.kw0 > 2) return 1;
     const bool bnb = a.flags & IG_BNBWD;
-    if (bnb && a.bnx2 && !a.bny) return 1;  // a second BN branch needs the mask from y (c2/c3 hold its constants)
+    if (bnb && a.bnx2 && !a.bnym) return 1;  // a second BN branch needs the output's mask bits (c2/c3 hold its constants)
     if (a.W == 56 && a.H % 4 == 0)
         return bnb ? launch_halo<56, 4, 1>(a, st) : launch_halo<56, 4, 0>(a, st);
     if (a.W == 112 && a.H % 2 == 0)

@@ -90,7 +90,7 @@ static void advance_images(IGemmArgs& t, const IGemmArgs& a, int i1) {
     t.X = a.X + i1 * xs;
     t.Y = static_cast<bf16_t*>(a.Y) + i1 * ys;  // staged epilogue: bf16 output only
     if (a.bnx) t.bnx = a.bnx + i1 * ys;
-    if (a.bny) t.bny = a.bny + i1 * ys;
+    if (a.bnym) t.bnym = a.bnym + i1 * ys / 8;
     if (a.bnx2) t.bnx2 = a.bnx2 + i1 * ys;
 }
 
@@ -103,7 +103,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (a.M <= 0 || a.Nout <= 0) return 0;
     if ((a.flags & IG_ACCUM) && (a.flags & IG_OUT_F32)) return -103;
     if ((a.flags & IG_BNBWD) && ((a.flags & (IG_OUT_F32 | IG_RELU)) || a.Nout % 8 || a.ldy != a.Nout || !a.bnx ||
-                                 !a.bnsave || !a.stats || (!a.bny && (!a.bngamma || !a.bnbeta)) ||
+                                 !a.bnsave || !a.stats || (!a.bnym && (!a.bngamma || !a.bnbeta)) ||
                                  (a.bnx2 && !a.bnsave2)))
         return -104;
     if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32

@@ -70,7 +70,9 @@ struct IGemmArgs {
     // IG_BNBWD: the BatchNorm this gradient flows into (all NHWC at the output
     // pixels, channel stride ldy == Nout)
     const bf16_t* bnx;     // BN input x
-    const bf16_t* bny;     // BN(+add)+ReLU output for the mask, or null: mask from x
+    // ReLU mask of the BN(+add)+ReLU output as bits (bn.hip bn_fwd ym: byte e/8 of element e, bit
+    // e%8 = output > 0; 1/16 of the bytes of re-reading the bf16 output), or null: mask from x
+    const uint8_t* bnym;
     const float* bnsave;   // [2][Nout] mean, rstd
     const float* bngamma;  // used with the from-x mask
     const float* bnbeta;
@@ -299,7 +301,7 @@ __device__ __forceinline__ void epilogue_tile(const IGemmArgs& a, const f32x4 (&
 
 // IG_BNBWD epilogue (dgrad whose output is the upstream gradient g of a
 // BatchNorm(+add)+ReLU), bf16 output with ldy == Nout, Nout % 8 == 0: the
-// stored value is the ReLU-masked g (mask from the saved output y, or
+// stored value is the ReLU-masked g (mask from the saved output's bit mask, or
 // recomputed from the BN input x as fma(x, sc, sh) > 0) and the slab
 // receives sum(g*xhat), sum(g) [, sum(g*xhat2)] (bn.hip row order), so the
 // separate reduce pass over (g, x, y) disappears.
@@ -311,7 +313,7 @@ template <int FN, int FM>
 __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], int nb, int mb,
                                              int lane, float* st) {
     const bool accum = a.flags & IG_ACCUM;
-    const bool has_y = a.bny != nullptr, has_x2 = a.bnx2 != nullptr;
+    const bool has_y = a.bnym != nullptr, has_x2 = a.bnx2 != nullptr;
     const int ohw = a.OH * a.OW;
     long pixo[FM];
     bool oldok[FM];
@@ -338,14 +340,16 @@ __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&a
             m2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + n);
             r2 = *reinterpret_cast<const f32x4*>(a.bnsave2 + a.Nout + n);
         }
-        u32x2 xw[FM], yw[FM], x2w[FM], ow[FM];
+        u32x2 xw[FM], x2w[FM], ow[FM];
+        uint32_t yw[FM];
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
-            xw[j] = yw[j] = x2w[j] = ow[j] = u32x2{0u, 0u};
+            xw[j] = x2w[j] = ow[j] = u32x2{0u, 0u};
+            yw[j] = 0u;
             if (pixo[j] < 0) continue;
             const size_t e = (size_t)pixo[j] + n;
             xw[j] = *reinterpret_cast<const u32x2*>(a.bnx + e);
-            if (has_y) yw[j] = *reinterpret_cast<const u32x2*>(a.bny + e);
+            if (has_y) yw[j] = (uint32_t)a.bnym[e >> 3] >> (e & 4);  // this lane's 4 channels
             if (has_x2) x2w[j] = *reinterpret_cast<const u32x2*>(a.bnx2 + e);
             if (oldok[j]) ow[j] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const bf16_t*>(a.Y) + e);
         }
@@ -361,10 +365,9 @@ __device__ __forceinline__ void epilogue_bnb(const IGemmArgs& a, const f32x4 (&a
                 v[0] += lo_bf(ow[j][0]); v[1] += hi_bf(ow[j][0]); v[2] += lo_bf(ow[j][1]); v[3] += hi_bf(ow[j][1]);
             }
             if (has_y) {
-                const float yv[4] = {lo_bf(yw[j][0]), hi_bf(yw[j][0]), lo_bf(yw[j][1]), hi_bf(yw[j][1])};
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (!(yv[r] > 0.f)) v[r] = 0.f;
+                    if (!((yw[j] >> r) & 1u)) v[r] = 0.f;
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -423,7 +426,7 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
     constexpr int NQ = BM / RG;     // chunks per thread
     static_assert(NT % CPR == 0 && BM % RG == 0, "epilogue split");
     const bool accum = a.flags & IG_ACCUM, bnb = a.flags & IG_BNBWD;
-    const bool has_y = bnb && a.bny, has_x2 = bnb && a.bnx2;
+    const bool has_y = bnb && a.bnym, has_x2 = bnb && a.bnx2;
     // this thread's fixed channel chunk (step 2); the forward-statistics shift is
     // loaded now so its latency hides behind step (1)
     const int cc = tid % CPR, rg = tid / CPR;
@@ -489,7 +492,8 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += QB) {
         long e[QB];
-        u32x4 xo[QB], yo[QB], x2o[QB], oo[QB];
+        u32x4 xo[QB], x2o[QB], oo[QB];
+        uint32_t yo[QB];
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
             const int row = rg + RG * (q0 + u);
@@ -506,7 +510,7 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 }
                 if (bnb) {
                     xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
-                    if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
+                    if (has_y) yo[u] = a.bnym[e[u] >> 3];
                     if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
                 }
             }
@@ -535,8 +539,7 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 }
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
-                    const bool keep = has_y ? ((c & 1 ? hi_bf(yo[u][c >> 1]) : lo_bf(yo[u][c >> 1])) > 0.f)
-                                            : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
+                    const bool keep = has_y ? ((yo[u] >> c) & 1u) : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
                     if (!keep) v[c] = 0.f;
                 }
             }

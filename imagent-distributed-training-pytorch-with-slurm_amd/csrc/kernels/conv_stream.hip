@@ -226,7 +226,8 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
             fetch(d, g + D * wstride);
             long e[NR];
-            u32x4 oo[NR], xo[NR], yo[NR], x2o[NR];
+            u32x4 oo[NR], xo[NR], x2o[NR];
+            uint32_t yo[NR];
             auto issue = [&](int u) {
                 const int m = g * 16 + u * PPR + lane / CH;
                 e[u] = m < a.M ? (long)m * a.ldy + n : -1;
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     }
                     if (bnb) {
                         xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
-                        if (has_y) yo[u] = *reinterpret_cast<const u32x4*>(a.bny + e[u]);
+                        if (has_y) yo[u] = a.bnym[e[u] >> 3];
                         if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
                     }
                 }
@@ -302,8 +303,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                         }
 #pragma unroll
                         for (int c = 0; c < 8; ++c) {
-                            const bool keep = has_y ? ((c & 1 ? hi_bf(yo[q][c >> 1]) : lo_bf(yo[q][c >> 1])) > 0.f)
-                                                    : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
+                            const bool keep = has_y ? ((yo[q] >> c) & 1u) : (fmaf(xv[c], sc[c], sh[c]) > 0.f);
                             if (!keep) v[c] = 0.f;
                         }
                     }
@@ -385,8 +385,8 @@ template <int K, int BN, int D>
 int launch_stream(const IGemmArgs& a, hipStream_t st) {
     if (!(a.flags & IG_BNBWD)) return launch_stream1<K, BN, D, 0>(a, st);
     if constexpr (BN <= 128) {
-        if (a.bnx2) return a.bny ? launch_stream1<K, BN, D, 3>(a, st) : 1;
-        return a.bny ? launch_stream1<K, BN, D, 1>(a, st) : launch_stream1<K, BN, D, 2>(a, st);
+        if (a.bnx2) return a.bnym ? launch_stream1<K, BN, D, 3>(a, st) : 1;
+        return a.bnym ? launch_stream1<K, BN, D, 1>(a, st) : launch_stream1<K, BN, D, 2>(a, st);
     }
     return 1;
 }
@@ -407,7 +407,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (a.X2) {  // folded BN backward (K = 2 x 256 -> 64 channels): this kernel or an error
         if (a.C != 512 || a.Nout != 64 || !(a.flags & IG_BNBWD) || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
             a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.H != a.OH || a.W != a.OW || a.ldy != a.Nout ||
-            a.ldb < a.C || (a.bnx2 && !a.bny))
+            a.ldb < a.C || (a.bnx2 && !a.bnym))
             return -110;
         static const int depth = [] {  // IMAGENT_FOLD_D: pixel groups prefetched per wave (A/B)
             const char* e = getenv("IMAGENT_FOLD_D");
@@ -477,7 +477,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // slices, plain epilogue
     if (a.C == 256 && a.Nout <= 128) {
         if (!(a.flags & IG_BNBWD)) return launch_stream1<256, 64, 2, 0>(a, st);
-        if (!a.bnx2) return a.bny ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
+        if (!a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
     }
     return 1;
 }

@@ -84,7 +84,7 @@ class IGemmArgs(C.Structure):
         ("YH", C.c_int), ("YW", C.c_int), ("sY", C.c_int), ("oy", C.c_int), ("ox", C.c_int),
         ("ldy", C.c_int),
         ("flags", C.c_int),
-        ("bnx", C.c_void_p), ("bny", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
+        ("bnx", C.c_void_p), ("bnym", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
         ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
         ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p), ("X2", C.c_void_p),
         ("xbn", C.c_void_p),
@@ -152,7 +152,7 @@ def _declare(name: str, lib) -> None:
             "imk_normalize_u8_f32": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_xent_bwd_f32": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
-                           vp],
+                           vp, vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],

@@ -161,6 +161,10 @@ class BlockFn(torch.autograd.Function):
         else:
             a = _fwd8(conv, h, h8, bn)
         q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
+        # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue (1/16
+        # of the bytes of re-reading the output there)
+        fuse_next = getattr(block, "_fuse_bnb", False)
+        ym = torch.empty(a.numel() // 8, device=a.device, dtype=torch.uint8) if fuse_next else None
         if ds is not None:
             if side is not None:
                 cur = torch.cuda.current_stream()
@@ -168,10 +172,10 @@ class BlockFn(torch.autograd.Function):
                 ad.record_stream(cur)  # allocated on the side stream, read / freed in main order
             else:
                 ad = _fwd8(ds[0], x, x8, ds[1])
-            out = bn_act_forward(a, ad, bn, ds[1], 2, True, q8=q8)
+            out = bn_act_forward(a, ad, bn, ds[1], 2, True, q8=q8, ym=ym)
         else:
             ad = None
-            out = bn_act_forward(a, x, bn, None, 1, True, q8=q8)
+            out = bn_act_forward(a, x, bn, None, 1, True, q8=q8, ym=ym)
         if q is not None:
             q.register(out, q8)
         saved += [a, ad, out]
@@ -181,7 +185,7 @@ class BlockFn(torch.autograd.Function):
             rows.append(ad.numel() // ad.shape[-1])
         block._bn_rows = rows
         # what the next block's backward needs to finish this block's last BN
-        block._last_bn = (a, ad, out) if getattr(block, "_fuse_bnb", False) else None
+        block._last_bn = (a, ad, ym) if fuse_next else None
         block._bnb_done = False
         ctx.block = block
         ctx.xbn = xbn
@@ -279,10 +283,10 @@ class BlockFn(torch.autograd.Function):
                 prev = getattr(block, "_prev_block", None)
                 fz = None
                 if fuse and prev is not None and prev._last_bn is not None:
-                    pa, pad_, pout = prev._last_bn
+                    pa, pad_, pym = prev._last_bn
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
-                    fz = BNBwdFuse(pa, pbn, y=pout, x2=pad_, bn2=pds[1] if pds is not None else None)
+                    fz = BNBwdFuse(pa, pbn, y=pym, x2=pad_, bn2=pds[1] if pds is not None else None)
                 if fold_done is not None:
                     torch.cuda.current_stream().wait_event(fold_done)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,

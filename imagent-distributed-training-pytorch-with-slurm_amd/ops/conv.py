@@ -50,7 +50,7 @@ def _igemm_call(a, tile: int, st, what: str) -> None:
     n0 = k.imk_conv_launches()
     _lib.check(k.imk_conv_igemm(C.byref(a), tile, st), what)
     _log(dict(op=what, N=a.N, H=a.H, W=a.W, C=a.C, OH=a.OH, OW=a.OW, M=a.M, Nout=a.Nout, taps=a.nth * a.ntw,
-              YH=a.YH, YW=a.YW, sY=a.sY, ldy=a.ldy, flags=a.flags, bnb=bool(a.flags & 32), y2=bool(a.bny),
+              YH=a.YH, YW=a.YW, sY=a.sY, ldy=a.ldy, flags=a.flags, bnb=bool(a.flags & 32), y2=bool(a.bnym),
               x2=bool(a.bnx2), stats=bool(a.stats), xbn=bool(a.xbn), X2=bool(a.X2)),
          k.imk_conv_launches() - n0, st)
 
@@ -247,9 +247,9 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
 class BNBwdFuse:
     """The BatchNorm a dgrad's output flows into (IG_BNBWD epilogue).
 
-    x: BN input; y: the saved BN(+add)+ReLU output for the mask (None: mask
-    recomputed from x with gamma/beta, plain BN+ReLU); x2/bn2: the downsample
-    BN branch of a fused residual (mode 2)."""
+    x: BN input; y: the ReLU mask of the BN(+add)+ReLU output as bits (uint8, numel / 8, written by the
+    forward's ``bn_act_forward(ym=)``; ``ops.bn.relu_mask_bits``), None: mask recomputed from x with
+    gamma/beta (plain BN+ReLU); x2/bn2: the downsample BN branch of a fused residual (mode 2)."""
 
     __slots__ = ("x", "y", "bn", "x2", "bn2")
 
@@ -261,7 +261,8 @@ class BNBwdFuse:
         a.flags |= 32
         a.stats = w.scratch.data_ptr()
         a.bnx = self.x.data_ptr()
-        a.bny = _lib.ptr(self.y)
+        assert self.y is None or self.y.dtype == torch.uint8, "BNBwdFuse.y: the ReLU mask bits"
+        a.bnym = _lib.ptr(self.y)
         a.bnsave = w.save.data_ptr()
         a.bngamma = self.bn.weight.data_ptr()
         a.bnbeta = self.bn.bias.data_ptr()

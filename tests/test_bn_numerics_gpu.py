@@ -56,3 +56,25 @@ def test_shifted_statistics_large_mean(Co):
           f"shifted -> mean err {errs[1][0]:.2e} sd, var rel err {errs[1][1]:.2e}")
     assert errs[1][0] < 1e-3, errs
     assert errs[1][1] < 1e-3, errs
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bn_fwd_relu_mask_bits(mode):
+    """bn_fwd's ReLU-mask bit output (ym) equals (y > 0) of the bf16 output it stores, packed as
+    ops.bn.relu_mask_bits -- the mask the next block's conv1 dgrad epilogue reads instead of y."""
+    from imagent_amd.models.resnet import BatchNorm2d
+    from imagent_amd.ops.bn import bn_fwd_launch, relu_mask_bits
+    torch.manual_seed(1)
+    N, H, C = 8, 14, 256
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    x2 = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    bn, bn2 = BatchNorm2d(C).to(DEV), BatchNorm2d(C).to(DEV)
+    stats = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5])
+    stats2 = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5])
+    y = torch.empty_like(x)
+    ym = torch.full((x.numel() // 8,), 0xA5, device=DEV, dtype=torch.uint8)
+    kw = dict(stats2=stats2, gamma2=bn2.weight, beta2=bn2.bias) if mode == 2 else {}
+    bn_fwd_launch(x, stats, bn.weight, bn.bias, y, None, x2=x2, mode=mode, relu=True, ym=ym, **kw)
+    torch.cuda.synchronize()
+    assert (y > 0).any() and (y == 0).any()
+    assert torch.equal(ym, relu_mask_bits(y))

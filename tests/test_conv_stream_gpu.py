@@ -80,6 +80,7 @@ def test_stream_dgrad_bnb_matches_tiled(shape, variant, stream_toggle):
     tiled kernel's (itself tested against PyTorch in test_model_gpu)."""
     from imagent_amd.models.resnet import BatchNorm2d, BNWork
     from imagent_amd.ops import _lib
+    from imagent_amd.ops.bn import relu_mask_bits
     from imagent_amd.ops.conv import BNBwdFuse, igemm_dgrad
     N, Co, H, Ci = shape  # conv Ci -> Co; the dgrad output has Ci channels
     torch.manual_seed(3)
@@ -106,7 +107,7 @@ def test_stream_dgrad_bnb_matches_tiled(shape, variant, stream_toggle):
         stream_toggle(stream)
         bn.work.scratch.zero_()
         out = old.clone() if old is not None else None
-        f = BNBwdFuse(x, bn, y=y, x2=x2, bn2=bn2 if x2 is not None else None)
+        f = BNBwdFuse(x, bn, y=relu_mask_bits(y) if y is not None else None, x2=x2, bn2=bn2 if x2 is not None else None)
         r = igemm_dgrad(dy, wt, (H, H), 1, 0, 1, 1, out=out, accumulate=old is not None, bnb=f)
         outs.append((r.clone(), bn.work.scratch[:32 * 3 * Ci].view(32, 3, Ci).sum(0).clone()))
     (r0, s0), (r1, s1) = outs
