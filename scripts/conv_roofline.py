@@ -8,7 +8,7 @@ dispatch ids follow the call order), steps are delimited by the fused SGD kernel
 
 Floors per call (the verdict's definitions): FLOP floor at the dense bf16 MFMA peak
 (2.5 PFLOP/s), byte floor at 8 TB/s over the operand bytes the call must move at least once
-(gathered input, weights, output; + the fused epilogue's operands: BN-backward x / y / x2, the
+(gathered input, weights, output; + the fused epilogue's operands: BN-backward x / y-mask bits / x2, the
 accumulated old output). "roof" = max of the two, "of roof" = roof / achieved, "above roof" =
 achieved - roof, the table is ranked by it (where the time is).
 
@@ -26,7 +26,7 @@ import sqlite3
 
 PEAK_FLOPS = 2.5e15
 PEAK_BYTES = 8e12
-CONV_KERNELS = ("igemm_", "conv_stream_kernel", "halo3x3_kernel", "wgrad_kernel")
+CONV_KERNELS = ("igemm_", "conv_stream_kernel", "halo3x3_kernel", "wgrad_kernel", "wgrad_v3_kernel")
 
 
 def flops_bytes(r):
@@ -44,8 +44,8 @@ def flops_bytes(r):
     by = xb + r["Nout"] * k * 2 + yb
     if r["flags"] & 8:  # accumulate: the old output is read
         by += yb
-    if r.get("bnb"):  # BN-backward epilogue reads x (+ y for the mask, + x2 of the second branch)
-        by += yb * (1 + r.get("y2", False) + r.get("x2", False))
+    if r.get("bnb"):  # BN-backward epilogue reads x (+ the output's ReLU mask bits, + x2 of the second branch)
+        by += yb * (1 + r.get("y2", False) / 16 + r.get("x2", False))
     return fl, by
 
 
