@@ -284,6 +284,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
 }  // namespace
 
 #include "conv_wgrad_v3.h"
+#include "conv_wgrad_halo.h"
 
 namespace {
 
@@ -383,6 +384,12 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
             default: return launch_wgrad_v3<64, 2>(a, splits, st);
         }
     }
+    // 64 -> 64 3x3 stride 1 at 56x56: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off
+    static const bool halo = [] {
+        const char* e = getenv("IMAGENT_WGRAD_HALO");
+        return !e || e[0] != '0';
+    }();
+    if (halo && wgrad_halo_ok(a)) return launch_wgrad_halo(a, st);
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
     // 2 % slower than this register-staged loop on every R50 shape: not kept)
@@ -392,7 +399,8 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
 }
 
 // explicit kernel choice (tests, A/B): -1 the register-staged kernel, 1..4 the v3 variants of
-// IMAGENT_WGRAD_V3 (-106 when the shape is not one v3 covers), 0 the default dispatch
+// IMAGENT_WGRAD_V3 (-106 when the shape is not one v3 covers), 9 the halo-tiled 64 -> 64 3x3 kernel,
+// 0 the default dispatch
 IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int variant, void* stream) {
     const WgradArgs& a = *args;
     if (variant == 0) return imk_conv_wgrad(args, splits, stream);
@@ -402,6 +410,7 @@ IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int var
         if (a.stem || a.dYx || a.xbn || a.Ci % 8 || a.Co % 8) return -106;
         return a.Co <= 64 ? launch<64, 128, 1, false>(a, splits, st) : launch<128, 128, 2, false>(a, splits, st);
     }
+    if (variant == 9) return wgrad_halo_ok(a) ? launch_wgrad_halo(a, st) : -106;
     if (!wgrad_v3_ok(a)) return -106;
     switch (variant) {
         case 1: return launch_wgrad_v3<64, 2>(a, splits, st);

@@ -1,0 +1,201 @@
+// Halo-tiled weight gradient of the 64 -> 64 3x3 stride-1 convs (ResNet stage 1 at 56x56; cuDNN's
+// conv wgrad inside loss.backward() in the reference, /root/reference/imagenet.py:128):
+//   dW[co][t][ci] += sum_p dY[p][co] * X[p + shift(t)][ci],   t = 3 ti + tj.
+//
+// The generic wgrad kernels tile K = 9 x 64 into 128-wide k tiles, so every input pixel is gathered
+// from L2 into LDS once per tap pair (4.5x) and the 64-row output tile leaves the MFMAs waiting on
+// the staging (404 TFLOP/s, profiles/r50_b1024_conv_shapes_v14.txt). Here, as in the forward halo
+// kernel (conv_halo.hip), a band of R output rows (R x W = 224 pixels) is staged ONCE:
+//   * dY band  [224 px][64 co] and the X patch [(R + 2) rows][PW px][64 ci] (band + 1-pixel halo,
+//     out-of-image pixels as zeros) land in LDS by LDS-DMA through buffer descriptors (out-of-range
+//     offsets read zeros), double-buffered: band n + 1 streams in while band n computes;
+//   * all 9 taps read the same patch as shifted windows;
+//   * wave w owns input channels 16w .. 16w + 15 for all 64 output channels and all 9 taps
+//     (36 accumulators of 16x16), so one k-step (32 pixels) is 4 dY fragments + 9 X fragments for
+//     36 MFMAs (v_mfma_f32_16x16x32_bf16, k = pixels);
+//   * fragments by ds_read_b64_tr_b16 (pixel rows -> k): a 32-lane half reads 8 consecutive pixel
+//     rows; rows are 128 B with 32-B segment s of row q stored at s ^ ((q >> 1) & 3), conflict-free
+//     for any 8 consecutive rows -- and because the patch pitch PW is a multiple of 8, shifting a
+//     window by a tap ROW keeps every row's swizzle, so the 3 tap rows share one address and an
+//     immediate offset (3 addresses per k-step and read instead of 9);
+//   * one persistent block per CU walks a contiguous range of bands; the 144 accumulators per lane
+//     leave with one fp32 atomic each into the gradient arena at the end.
+// Shapes (host): Ci = Co = 64, KH = KW = 3, stride 1, pad 1, W = 56, H % R == 0, no operand BN.
+
+#pragma once
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr uint32_t WH_OOB = 0x80000000u;
+
+__device__ __forceinline__ int wh_swz(int q) { return (q >> 1) & 3; }
+
+// physical 16-B chunk slot of logical chunk c (0..7) of row q (and its inverse: the map is an involution)
+__device__ __forceinline__ int wh_slot(int c, int q) { return (((c >> 1) ^ wh_swz(q)) << 1) | (c & 1); }
+
+template <int W, int R>
+__global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, int nbands) {
+    constexpr int BP = R * W;          // band pixels
+    constexpr int NKS = BP / 32;       // MFMA k-steps per band
+    constexpr int PW = 64;             // patch pitch (pixels): multiple of 8, >= W + 2
+    constexpr int PR = R + 2;          // patch rows
+    constexpr int DYB = BP * 128;      // dY image bytes
+    constexpr int PB = PR * PW * 128;  // patch image bytes
+    constexpr int BUF = DYB + PB;
+    constexpr int NDY = DYB / 1024, NPA = PB / 1024;
+    constexpr int PPW = (NDY + NPA) / 4;  // DMA pieces per wave per band
+    static_assert(W + 2 <= PW && BP % 32 == 0 && W % 8 == 0 && (NDY + NPA) % 4 == 0, "band geometry");
+    static_assert(2 * BUF <= 160 * 1024, "two band buffers in LDS");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int G = gridDim.x;
+    const int lid = xcd_remap(blockIdx.x, G);
+    const int b0 = (int)((long)nbands * lid / G), b1 = (int)((long)nbands * (lid + 1) / G);
+    if (b0 >= b1) return;  // whole block
+    const int bpi = a.H / R;
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.dY), (short)0, (int)((size_t)a.M * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(a.X), (short)0, (int)((size_t)a.N * a.H * W * 128), 0x00020000);
+
+    // ---- DMA of band `band` into buffer `buf`: piece k of this wave = LDS rows 8k' .. 8k' + 7,
+    // lane -> (row (lane >> 3), slot lane & 7), source chunk = slot's logical chunk
+    const int drow = lane >> 3, dslot = lane & 7;
+    auto issue_band = [&](int band, int buf) {
+        const int img = band / bpi, y0 = (band - img * bpi) * R;
+        const uint32_t pix0 = (uint32_t)((img * a.H + y0) * W);  // band's first pixel
+#pragma unroll
+        for (int k = 0; k < PPW; ++k) {
+            const int piece = wid * PPW + k;
+            char* lds = smem + buf * BUF + piece * 1024;
+            if (piece < NDY) {
+                const int row = piece * 8 + drow;
+                const uint32_t off = (pix0 + (uint32_t)row) * 128u + (uint32_t)(wh_slot(dslot, row) * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (__attribute__((address_space(3))) void*)lds, 16, off, 0,
+                                                         0, 0);
+            } else {
+                const int q = (piece - NDY) * 8 + drow;  // patch row index
+                const int pr = q / PW, pc = q - pr * PW;
+                const int iy = y0 - 1 + pr, ix = pc - 1;
+                uint32_t off = WH_OOB;
+                if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)W)
+                    off = ((uint32_t)(img * a.H + iy) * W + (uint32_t)ix) * 128u + (uint32_t)(wh_slot(dslot, q) * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)lds, 16, off, 0,
+                                                         0, 0);
+            }
+        }
+    };
+
+    // ---- fragment addresses (band-invariant, relative to the buffer base): lane 4q + p of its 16-lane
+    // group reads row q of a 4-row block, columns 4p .. 4p + 3 of a 16-channel (32-B) segment; the
+    // 32-lane half h reads rows 8 (2 r + h) + 4 g + q of k-step ks in read r (g = group within the half)
+    const int h = lane >> 5, g = (lane >> 4) & 1, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    uint32_t adA[NKS][2][4], adB[NKS][2][3];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int P = ks * 32 + (2 * r + h) * 8 + 4 * g + q4;  // band pixel
+#pragma unroll
+            for (int i = 0; i < 4; ++i) adA[ks][r][i] = (uint32_t)(P * 128 + ((i ^ wh_swz(P)) << 5) + 8 * p4);
+            const int Q0 = (P / W) * PW + (P % W);  // patch row of tap (0, 0)
+#pragma unroll
+            for (int tj = 0; tj < 3; ++tj) {
+                const int q = Q0 + tj;
+                adB[ks][r][tj] = (uint32_t)(DYB + q * 128 + ((wid ^ wh_swz(q)) << 5) + 8 * p4);
+            }
+        }
+
+    f32x4 acc[4][9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue_band(b0, 0);
+    if (b0 + 1 < b1) issue_band(b0 + 1, 1);
+    for (int band = b0; band < b1; ++band) {
+        const int buf = (band - b0) & 1;
+        // this band's pieces have landed (the next band's PPW may still be in flight), in every wave
+        if (band + 1 < b1)
+            __builtin_amdgcn_s_waitcnt((PPW & 0xF) | ((PPW >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+        else
+            __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+        __builtin_amdgcn_s_barrier();
+        const char* base = smem + buf * BUF;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            bf16x8 fa[4], fb[9];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(base + adA[ks][0][i]));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(base + adA[ks][1][i]));
+                fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int ti = 0; ti < 3; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 3; ++tj) {
+                    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (LDS_PTR(s16x4))(base + adB[ks][0][tj] + ti * PW * 128));
+                    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (LDS_PTR(s16x4))(base + adB[ks][1][tj] + ti * PW * 128));
+                    fb[ti * 3 + tj] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[t], acc[i][t], 0, 0, 0);
+        }
+        // every wave is done reading this buffer before band + 2 overwrites it
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only (vmcnt 63, expcnt 7)
+        __builtin_amdgcn_s_barrier();
+        if (band + 2 < b1) issue_band(band + 2, buf);
+    }
+
+    // acc[i][t][r]: co = 16 i + 4 (lane >> 4) + r, k = 64 t + 16 wid + (lane & 15)
+    const int K = 9 * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float* dst = a.dW + (size_t)(16 * i + 4 * (lane >> 4) + r) * K + 16 * wid + (lane & 15);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) atomicAdd(dst + 64 * t, acc[i][t][r]);
+        }
+}
+
+// the shapes this kernel covers (host)
+inline bool wgrad_halo_ok(const WgradArgs& a) {
+    if (a.stem || a.dYx || a.xbn) return false;
+    if (a.Ci != 64 || a.Co != 64 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1) return false;
+    if (a.W != 56 || a.OW != 56 || a.OH != a.H || a.H % 4 != 0) return false;
+    return (size_t)a.N * a.H * a.W * 128 < (1ull << 31);
+}
+
+inline int launch_wgrad_halo(const WgradArgs& a, hipStream_t st) {
+    constexpr int W = 56, R = 4;
+    const int nbands = a.N * (a.H / R);
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    const int grid = std::min(nbands, cus);
+    const size_t lds = 2 * ((size_t)R * W * 128 + (size_t)(R + 2) * 64 * 128);
+    hipLaunchKernelGGL((wgrad_halo_kernel<W, R>), dim3(grid), dim3(256), lds, st, a, nbands);
+    CONV_COUNTED();
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace

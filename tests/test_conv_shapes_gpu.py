@@ -62,6 +62,7 @@ BENCH_KERNELS = [
     "wgrad_kernel<64, 128, 1, false, 4, 32, false, false>",
     "wgrad_kernel<64, 128, 1, true, 4, 32, false, false>",
     "wgrad_v3_kernel<64, 2>",
+    "wgrad_halo_kernel<56, 4>",
 ]
 
 
@@ -76,7 +77,7 @@ def _kernels(fn):
         out = fn()
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
-    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_kernel", "wgrad_v3_kernel", "halo3x3"))]
+    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_", "halo3x3"))]
 
 
 def _short(names):
