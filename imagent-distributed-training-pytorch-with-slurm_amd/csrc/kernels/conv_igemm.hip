@@ -12,8 +12,9 @@
 //    (round-3 A/B at R50 / 1024 img, profiles/r50_b1024_conv_v3.md);
 //  * the rest (C % 64 != 0, direct epilogues, Nout <= 64): the LDS-DMA ring / register-staged
 //    kernels of conv_igemm_impl.h.
-// Explicit tiles (A/B, tests): 1-9 ring / register-staged variants, 17 / 18 v3 256x256 / 128x128,
-// 23-27 v3 tile / ring-depth variants (256x128, 128x256, 128x128 x3, 128x128 BK32 x4, 256x256 BK32 x4).
+// Explicit tiles (A/B, tests): 1-9 ring / register-staged variants, 17 / 18 v3 256x256 / 128x128.
+// Measured and removed in round 3 (profiles/r50_b1024_v3_tile_study.md): v3 at 256x128, 128x256, 3-deep,
+// and BK-32 4-deep rings, and a ping-pong 256x256 schedule with v3 addressing -- all within 2 % of v3.
 // Measured slower and removed in round 3: the phased 256x256 kernel (profiles/
 // r50_conv_phased_kernel.md), the ping-pong 256x256 kernel after the 8-phase template (-3.2 %),
 // static wave priority for the second half of the waves (neutral).
@@ -163,17 +164,9 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
-    if (tile == 17 || tile == 18 || (tile >= 23 && tile <= 27)) {  // v3 main loop (conv_igemm_v3.h)
+    if (tile == 17 || tile == 18) {  // v3 main loop (conv_igemm_v3.h)
         if (!use_lds || !v3_ok(a)) return -105;
-        switch (tile) {  // 23-27: tile / ring-depth study (conv_bench.py --tiles)
-            case 17: return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
-            case 23: return launch_v3<256, 128, 2, 2, 8, 128>(a, st);
-            case 24: return launch_v3<128, 256, 4, 2, 8, 128>(a, st);
-            case 25: return launch_v3<128, 128, 2, 3, 4, 128>(a, st);
-            case 26: return launch_v3<128, 128, 2, 4, 4, 64>(a, st);
-            case 27: return launch_v3<256, 256, 2, 4, 8, 64>(a, st);
-            default: return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
-        }
+        return tile == 17 ? launch_v3<256, 256, 2, 2, 8, 128>(a, st) : launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
