@@ -217,6 +217,27 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     }
 }
 
+// inference BatchNorm as the conv epilogue's per-channel [scale; shift] (IG_AFFINE), for every BN of the
+// model in ONE launch over a descriptor table (models/native.py _forward_eval): out = [g rstd; b - mean g rstd]
+struct AffDesc {
+    const float* gamma;
+    const float* beta;
+    const float* rmean;
+    const float* rvar;
+    float* out;
+    int C;
+    float eps;
+};
+
+__global__ void bn_eval_affine_kernel(const AffDesc* __restrict__ d, int n) {
+    const AffDesc a = d[blockIdx.x];
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+        const float sc = a.gamma[c] * rsqrtf(a.rvar[c] + a.eps);
+        a.out[c] = sc;
+        a.out[a.C + c] = a.beta[c] - a.rmean[c] * sc;
+    }
+}
+
 // running stats update + num_batches_tracked: all layers of a step are updated
 // by ONE launch over a descriptor table (imk_bn_running_update)
 struct RunDesc {
@@ -566,6 +587,14 @@ IMK_EXPORT int imk_bn_running_update(const void* descs, int n, void* stream) {
 }
 
 IMK_EXPORT int imk_bn_rundesc_size() { return (int)sizeof(RunDesc); }
+
+IMK_EXPORT int imk_bn_eval_affine(const void* descs, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(bn_eval_affine_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, (const AffDesc*)descs, n);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+IMK_EXPORT int imk_bn_affdesc_size() { return (int)sizeof(AffDesc); }
 
 // Apply-only backward for a gradient g that the producing dgrad already
 // ReLU-masked, with its reductions already in the [BWD_SLOTS][3][C] slab of

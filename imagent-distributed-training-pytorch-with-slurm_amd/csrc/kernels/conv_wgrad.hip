@@ -384,12 +384,13 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
             default: return launch_wgrad_v3<64, 2>(a, splits, st);
         }
     }
-    // 64 -> 64 3x3 stride 1 at 56x56: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off
-    static const bool halo = [] {
+    // 3x3 stride 1 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
+    // 1 only 64 -> 64, 2 (default) every shape it covers
+    static const int halo = [] {
         const char* e = getenv("IMAGENT_WGRAD_HALO");
-        return !e || e[0] != '0';
+        return e ? atoi(e) : 2;
     }();
-    if (halo && wgrad_halo_ok(a)) return launch_wgrad_halo(a, st);
+    if (halo && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
     // 2 % slower than this register-staged loop on every R50 shape: not kept)

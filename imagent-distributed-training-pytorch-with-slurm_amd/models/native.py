@@ -154,6 +154,26 @@ class NativeState:
         self._run_descs = descs
         self.bns = bns
 
+    def eval_affines(self) -> None:
+        """Every BN's inference [scale; shift] (``bn._eval_aff``, the conv epilogue's IG_AFFINE operand) from the
+        current weights / running statistics: one launch over a descriptor table per eval forward."""
+        if getattr(self, "_aff_dev", None) is None:
+            sizes = [bn.num_features for bn in self.bns]
+            self._aff_buf = torch.empty(sum(2 * c for c in sizes), dtype=torch.float32, device=self.device)
+            descs = (_lib.AffDesc * len(self.bns))()
+            o = 0
+            for d, bn in zip(descs, self.bns):
+                c = bn.num_features
+                bn._eval_aff = self._aff_buf[o:o + 2 * c].view(2, c)
+                d.gamma, d.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
+                d.rmean, d.rvar = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+                d.out, d.C, d.eps = bn._eval_aff.data_ptr(), c, bn.eps
+                o += 2 * c
+            raw = bytes(memoryview(descs))
+            self._aff_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        _lib.check(_lib.kernels().imk_bn_eval_affine(self._aff_dev.data_ptr(), len(self.bns), _lib.stream_ptr()),
+                   "bn eval affine")
+
     def running_update(self, rows: List[int]) -> None:
         """After a training forward: update every BN's running stats in one launch."""
         key = tuple(rows)
@@ -343,9 +363,15 @@ def _forward_eval(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     of the conv that feeds it -- one pass per conv, no BN kernels.
     The block's last conv accumulates onto the shortcut (identity copy or the
     downsample conv's folded output) and applies the ReLU after the sum."""
+    st = getattr(model, "native", None)
+    st = st if isinstance(st, NativeState) else None
+    if st is not None:
+        st.eval_affines()  # bn._eval_aff for every BN, one launch
+
     def conv(h, c, bn, relu, out=None, accumulate=False):
+        aff = bn._eval_aff if st is not None else _affine(bn)
         return igemm_fwd(h, c.w_bf16, c.stride, c.padding, c.kh, c.kw, stem=getattr(c, "stem", False),
-                         affine=_affine(bn), relu=relu, out=out, accumulate=accumulate)
+                         affine=aff, relu=relu, out=out, accumulate=accumulate)
 
     y = conv(x, model.conv1, model.bn1, True)
     y = maxpool_eval(y, 3, 2, 1)
@@ -355,10 +381,9 @@ def _forward_eval(model: ResNet, x: torch.Tensor) -> torch.Tensor:
         for c, bn, _ in pairs[:-1]:
             h = conv(h, c, bn, True)
         c, bn, _ = pairs[-1]
-        if b.downsample is not None:
-            short = conv(y, b.downsample[0], b.downsample[1], False)
-        else:
-            short = y.clone()
+        # the block's last conv accumulates onto the shortcut: the downsample conv's output, or the block
+        # input itself, in place (no later reader: every consumer of y in this block has run)
+        short = conv(y, b.downsample[0], b.downsample[1], False) if b.downsample is not None else y
         y = conv(h, c, bn, True, out=short, accumulate=True)
     pooled = _avg_eval(y)
     fc = model.fc

@@ -122,6 +122,13 @@ class RunDesc(C.Structure):
     ]
 
 
+class AffDesc(C.Structure):
+    _fields_ = [
+        ("gamma", C.c_void_p), ("beta", C.c_void_p), ("rmean", C.c_void_p), ("rvar", C.c_void_p),
+        ("out", C.c_void_p), ("C", C.c_int), ("eps", C.c_float),
+    ]
+
+
 class TDesc(C.Structure):
     _fields_ = [
         ("src", C.c_void_p), ("dst", C.c_void_p),
@@ -156,6 +163,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],
+            "imk_bn_eval_affine": [vp, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, vp, i32, i32, i64, vp],
             "imk_bn_finalize_affine": [vp, vp, vp, vp, vp, vp, i32, i32, i64, f32, i32, vp],
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
@@ -175,7 +183,7 @@ def _declare(name: str, lib) -> None:
             "imk_cast_bf16": [vp, vp, i64, vp],
             "imk_normalize_u8": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_transpose_batched": [vp, i32, i32, vp],
-            "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [],
+            "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [], "imk_bn_affdesc_size": [],
             "imk_tdesc_size": [], "imk_bn_bwd_scratch_floats": [i32],
             "imk_quant_fp8": [vp, vp, i64, vp, vp, vp],
             "imk_fp8_update_exp": [vp, vp, i32, i32, vp],
@@ -189,7 +197,7 @@ def _declare(name: str, lib) -> None:
             f.restype = C.c_int
         # ABI guard: the ctypes mirrors must match the compiled structs
         for fn, st in [("imk_igemm_args_size", IGemmArgs), ("imk_wgrad_args_size", WgradArgs),
-                       ("imk_bn_rundesc_size", RunDesc), ("imk_tdesc_size", TDesc),
+                       ("imk_bn_rundesc_size", RunDesc), ("imk_bn_affdesc_size", AffDesc), ("imk_tdesc_size", TDesc),
                        ("imk_qdesc_size", QDesc), ("imk_lars_desc_size", LarsDesc)]:
             n = getattr(lib, fn)()
             if n != C.sizeof(st):

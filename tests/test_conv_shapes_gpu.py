@@ -62,7 +62,9 @@ BENCH_KERNELS = [
     "wgrad_kernel<64, 128, 1, false, 4, 32, false, false>",
     "wgrad_kernel<64, 128, 1, true, 4, 32, false, false>",
     "wgrad_v3_kernel<64, 2>",
-    "wgrad_halo_kernel<56, 4>",
+    "wgrad_halo_kernel<14, 14, 7, 16>",
+    "wgrad_halo_kernel<28, 4, 4, 32>",
+    "wgrad_halo_kernel<56, 4, 7, 64>",
 ]
 
 

@@ -210,24 +210,25 @@ def test_wgrad_v3(shape, variant):
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
 
 
-@pytest.mark.parametrize("N,H", [(3, 56), (5, 8), (1, 4)])
-def test_wgrad_halo_64(N, H):
-    """Halo-tiled 64 -> 64 3x3 weight gradient (conv_wgrad_halo.h, variant 9) against the fp32 conv
-    weight gradient: image borders on every side, bands crossing images (N * H / 4 bands spread over up
-    to 256 blocks, one band per block at the smallest shape), and the default dispatch picks it."""
+@pytest.mark.parametrize("N,Ci,Co,H,W", [(3, 64, 64, 56, 56), (5, 64, 64, 8, 56), (1, 64, 64, 4, 56),
+                                         (3, 128, 128, 28, 28), (2, 64, 192, 8, 28), (2, 256, 256, 14, 14),
+                                         (3, 128, 64, 14, 14), (3, 512, 512, 7, 7), (1, 64, 128, 7, 7)])
+def test_wgrad_halo(N, Ci, Co, H, W):
+    """Halo-tiled 3x3 weight gradient (conv_wgrad_halo.h, variant 9) against the fp32 conv weight gradient:
+    64-channel co / ci slices, image borders on every side, bands crossing images, zero-padded k rows
+    (W 28 / 14 / 7), more ranges than bands; the default dispatch picks it; += semantics."""
     from imagent_amd.ops.conv import igemm_wgrad
     torch.manual_seed(11)
-    x = bf(torch.randn(N, 64, H, 56, device=DEV))
-    w = torch.randn(64, 64, 3, 3, device=DEV).requires_grad_(True)
+    x = bf(torch.randn(N, Ci, H, W, device=DEV))
+    w = torch.randn(Co, Ci, 3, 3, device=DEV).requires_grad_(True)
     yr = F.conv2d(x.float(), w, None, 1, 1)
     g = bf(torch.randn_like(yr))
     yr.backward(g.float())
-    for variant in (9, 0):
-        dw = torch.zeros(64, 3, 3, 64, device=DEV)
+    for variant in (9, 0):  # (the default dispatch keeps W 7 on the register-staged kernel)
+        dw = torch.zeros(Co, 3, 3, Ci, device=DEV)
         igemm_wgrad(nhwc(g), nhwc(x), dw, 1, 1, 3, 3, variant=variant)
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, variant
-    dw0 = torch.zeros(64, 3, 3, 64, device=DEV)  # accumulates (+=) into the gradient
-    dw0 += 1.0
+    dw0 = torch.ones(Co, 3, 3, Ci, device=DEV)  # accumulates (+=) into the gradient
     igemm_wgrad(nhwc(g), nhwc(x), dw0, 1, 1, 3, 3, variant=9)
     assert rel(dw0.permute(0, 3, 1, 2) - 1.0, w.grad) < 5e-3
 
