@@ -94,6 +94,8 @@ def main(argv=None):
     ap.add_argument("--eval", type=int, default=0,
                     help="N > 0: after the timed training steps, also time N validation steps (the folded-BN eval "
                          "forward + loss + top-k counters, imagenet.py:166-210) and report val_img_s")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="1: BatchNorm statistics without float atomics (fixed-order passes; ops/conv.py)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
                     help="fp8: e4m3 forward convs (block-scaled MFMA), bf16 backward; fp32: the reference's own "
                          "precision (imagenet.py:312 trains fp32): exact-f32 MFMA kernels with --kernels hip "
@@ -168,6 +170,9 @@ def main(argv=None):
             arena = native.arena
         elif a.kernels == "hip":
             from imagent_amd.models.native import bind_native
+            if a.deterministic:
+                from imagent_amd.ops.conv import set_deterministic
+                set_deterministic(True)
             native = bind_native(model, dev, order, bnb_fusion=bool(a.bn_fusion), fp8=a.dtype == "fp8",
                                  wgrad_overlap=bool(a.wgrad_overlap))
             arena = native.arena
@@ -284,6 +289,7 @@ def main(argv=None):
                     "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip" and not f32_hip,
                     "auto_batch_reduced": auto_reduced,
                     "bucket_mb": a.bucket_mb,
+                    "deterministic": bool(a.deterministic),
                     "mean_train_loss": round(loss, 4),
                     "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
                     "reserved_hbm_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1)

@@ -33,6 +33,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet34", "resnet50", "resnet101",
                                                            "resnet152"])
     p.add_argument("--image-size", type=int, default=448)
+    p.add_argument("--deterministic", action="store_true",
+                   help="BatchNorm statistics without float atomics (fixed-order reduction passes): two runs "
+                        "from the same state give bit-identical statistics (HIP kernels)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
                    help="compute dtype. HIP kernels: bf16 (fp32 masters/accumulation), or fp8 = e4m3 "
                         "forward convs on the block-scaled MFMA with bf16 backward; fp32 = torch oracle path")

@@ -23,6 +23,8 @@
 // 16-B chunk (8 channels) of a row -> per-thread channel constants live in
 // registers, loads/stores are 16 B per lane (cdna_hip_programming.md G13).
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -217,6 +219,73 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     }
 }
 
+// ---------------------------------------------------------------- deterministic mode
+// IMAGENT_DETERMINISTIC=1 (ops/conv.py set_deterministic): batch statistics without float atomics, so two
+// passes over the same data give bit-identical BatchNorm statistics (and everything downstream of them).
+// Forward: the conv runs without its epilogue statistics and this pass reads its output: per-thread sums
+// over a fixed row sequence, a fixed-order fold of the block's rows in LDS, one plain store per channel
+// into the block's own partial row, then det_fold_kernel adds the rows in block order into slot 0 of the
+// BN's slab. Backward: bn_bwd_reduce_kernel with `partial` (the same fold). Same statistics as the
+// epilogue path (shifted sums around work.save, imk_bn_stats_finalize), different summation order.
+__global__ __launch_bounds__(256) void bn_stats_det_kernel(const bf16_t* __restrict__ y, const float* __restrict__ shift,
+                                                           float* __restrict__ partial, long R, int C) {
+    __shared__ float red[2048];  // [rpb][C]
+    const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
+    const bool active = tid < rpb * cpr;
+    const int c0 = (tid % cpr) * 8, rsub = tid / cpr;
+    float sh[8], s1[8], s2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        sh[i] = shift ? shift[c0 + i] : 0.f;
+        s1[i] = s2[i] = 0.f;
+    }
+    if (active) {
+        const long step = (long)gridDim.x * rpb;
+        for (long r0 = (long)blockIdx.x * rpb + rsub; r0 < R; r0 += U * step) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ldw(y + (size_t)min(r0 + u * step, R - 1) * C + c0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (r0 + u * step >= R) break;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float d = bfw(v[u], i) - sh[i];
+                    s1[i] += d;
+                    s2[i] += d * d;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) red[rsub * C + c0 + i] = q ? s2[i] : s1[i];
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            float t = 0.f;
+            for (int rr = 0; rr < rpb; ++rr) t += red[rr * C + c];
+            partial[(size_t)blockIdx.x * 2 * C + q * C + c] = t;
+        }
+    }
+}
+
+// out[i] += sum over b = 0 .. nb - 1 (in that order) of partial[b * stride + i], i < n
+__global__ void det_fold_kernel(const float* __restrict__ partial, int nb, int stride, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += partial[(size_t)b * stride + i];
+    out[i] += s;
+}
+
+int g_det = 0;            // deterministic mode (imk_set_deterministic)
+float* g_det_ws = nullptr;  // BN-backward partial rows (main stream only): <= 1024 blocks x 3 x 2048 channels
+constexpr size_t DET_WS_FLOATS = (size_t)1024 * 3 * 2048;
+
 // inference BatchNorm as the conv epilogue's per-channel [scale; shift] (IG_AFFINE), for every BN of the
 // model in ONE launch over a descriptor table (models/native.py _forward_eval): out = [g rstd; b - mean g rstd]
 struct AffDesc {
@@ -348,7 +417,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
     const bf16_t* __restrict__ x2, const float* __restrict__ save2, float* __restrict__ scratch, long R,
-    int C) {
+    int C, float* __restrict__ partial) {
     __shared__ float red[2048];  // [rpb][C], rpb*C == 2048
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
     const bool active = tid < rpb * cpr;
@@ -413,11 +482,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         // one add per channel per block into slot (block & 31) of the [32][3][C]
         // slab: 1024 blocks adding into the same 3*C words serialise at the
         // memory-side atomic unit (the conv-epilogue statistics lesson)
+        // (deterministic mode: a plain store into this block's own row of `partial`, folded in block order)
         float* slot = scratch + (size_t)(blockIdx.x & (BWD_SLOTS - 1)) * 3 * C;
         for (int c = tid; c < C; c += 256) {
             float s = 0.f;
             for (int rr = 0; rr < rpb; ++rr) s += red[rr * C + c];
-            atomicAdd(slot + qi * C + c, s);
+            if (partial)
+                partial[(size_t)blockIdx.x * 3 * C + qi * C + c] = s;
+            else
+                atomicAdd(slot + qi * C + c, s);
         }
     }
 }
@@ -715,6 +788,32 @@ IMK_EXPORT int imk_bnfold_weights(const void* wt, int ldw, const float* coef, vo
 IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 3) * C; }
 
 // forward statistics: shifted-sum slab [S][2][C] -> out [2][C] = (mean, biased variance)
+// deterministic mode on / off; on: allocates the partial-row workspace once (no allocation inside a capture)
+IMK_EXPORT int imk_set_deterministic(int on) {
+    if (on && !g_det_ws && hipMalloc(&g_det_ws, DET_WS_FLOATS * sizeof(float)) != hipSuccess) return -1;
+    g_det = on ? 1 : 0;
+    return 0;
+}
+
+// forward BatchNorm statistics of y [R][C] (bf16) as shifted sums around `shift` (or raw sums) added to
+// slot 0 of the [S][2][C] slab, in a fixed summation order (deterministic mode). `partial`: the caller's
+// stream-ordered workspace of imk_bn_stats_det_floats(R, C) floats (the downsample conv's statistics run on
+// the side stream beside the main chain's, so no shared scratch here)
+IMK_EXPORT long imk_bn_stats_det_floats(long R, int C) { return (long)std::min(grid_for(R, C), 2048) * 2 * C; }
+
+IMK_EXPORT int imk_bn_stats_det(const void* y, const float* shift, float* slab, float* partial, long R, int C,
+                                void* stream) {
+    if (C % 8 || C > 2048 || R <= 0 || !partial) return -100;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = std::min(grid_for(R, C), 2048);
+    hipLaunchKernelGGL(bn_stats_det_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)y, shift, partial, R, C);
+    IMK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(det_fold_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, partial, grid, 2 * C, 2 * C,
+                       slab);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
 IMK_EXPORT int imk_bn_stats_finalize(const float* slab, const float* shift, float* out, int S, int C, long R,
                                      void* stream) {
     if (R <= 0) return -100;
@@ -751,11 +850,17 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
 #define LR(MK, M)                                                                                  \
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<MK, M>), dim3(rgrid), dim3(256), 0, st,               \
                        (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta,    \
-                       (const bf16_t*)x2, save2, scratch, R, C)
+                       (const bf16_t*)x2, save2, scratch, R, C, det)
+    float* det = g_det ? g_det_ws : nullptr;
     if (mode == 2) { if (relu) LR(1, 2); else LR(0, 2); }
     else { if (relu == 2) LR(2, 0); else if (relu) LR(1, 0); else LR(0, 0); }
 #undef LR
     IMK_CHECK_LAUNCH();
+    if (det) {  // the blocks' rows in block order into slot 0
+        const int n = (mode == 2 ? 3 : 2) * C;  // the quantities this mode reduces
+        hipLaunchKernelGGL(det_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, st, det, rgrid, 3 * C, n, scratch);
+        IMK_CHECK_LAUNCH();
+    }
     float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
     hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
                        BWD_SLOTS, 3 * C);

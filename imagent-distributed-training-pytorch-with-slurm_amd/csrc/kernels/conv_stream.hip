@@ -445,21 +445,26 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     }
     int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (a.flags & IG_BNBWD) {
-        // BN-backward epilogue: IMAGENT_STREAM_BNB = 0 (never), 64 / 128 (slice width)
+        // BN-backward epilogue: IMAGENT_STREAM_BNB = all (default: every K = 64 / 128 / 256 dgrad, with or
+        // without the second BN branch), 0 (never), 64 / 128 (slice width; K = 64 / 256 without the second
+        // branch only), x2 (the latter + K = 64 with the second branch). Same-box bench A/B at R50 / 1024 with
+        // the ReLU mask as bits (round 3): all 73.9 ms/step vs 75.2 for 128 and 75.0 for x2 (the round-1
+        // measurement that kept K = 128 and the second branch on the tiled kernels predates the bit mask
+        // and the register-light BN epilogue)
         static const int pref = [] {
             const char* e = getenv("IMAGENT_STREAM_BNB");
-            return e ? atoi(e) : 128;
+            return !e || e[0] == 'a' || e[0] == 'x' ? 128 : atoi(e);
         }();
         if (pref == 0) return 1;
-        // measured in the R50 step (profiles/r50_b512_v6): the tiled kernels'
-        // staged BN-backward epilogue wins for K = 128 (535 vs 622 us) and
-        // with the second BN branch (1037 vs 1097 us); this kernel for K = 64
-        // with the y mask (893 vs 916 us). IMAGENT_STREAM_BNB=all: every case.
         static const bool all = [] {
             const char* e = getenv("IMAGENT_STREAM_BNB");
-            return e && e[0] == 'a';
+            return !e || e[0] == 'a';
         }();
-        if (!all && ((a.C != 64 && a.C != 256) || a.bnx2)) return 1;
+        static const bool x2 = [] {
+            const char* e = getenv("IMAGENT_STREAM_BNB");
+            return e && e[0] == 'x';
+        }();
+        if (!all && ((a.C != 64 && a.C != 256) || (a.bnx2 && !(x2 && a.C == 64)))) return 1;
         maxbn = (pref >= 128 || all) ? 128 : 64;
     }
     if (bn == 0) bn = maxbn;

@@ -23,7 +23,7 @@ import torch
 from ..ops import _lib
 from ..ops.block import BlockFn
 from ..ops.bn import BNActFn, bn_eval, running_update
-from ..ops.conv import ConvFn, LinearFn, igemm_fwd
+from ..ops.conv import ConvFn, LinearFn, deterministic, igemm_fwd
 from ..ops.misc import AvgPoolFn, BNReluPoolFn, MaxPoolFn, TransposePlan, maxpool_eval
 from .arena import ParamArena
 from .resnet import BasicBlock, BatchNorm2d, BNWork, Bottleneck, Conv2d, Linear, ResNet
@@ -47,6 +47,8 @@ class NativeState:
         self.fused_blocks = True
         # BN-backward reductions folded into the producing dgrad's (LDS-staged,
         # coalesced) epilogue (ops/block.py): +11 % img/s at 512 img/GPU
+        # deterministic mode: BN-backward reductions by the fixed-order reduce pass, not the dgrad epilogues
+        bnb_fusion = bnb_fusion and not deterministic()
         self.bnb_fusion = bnb_fusion
         blocks = list(model.blocks())
         for k, b in enumerate(blocks):
@@ -304,7 +306,7 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     rows = []
     y = _conv(x, model.conv1, model.bn1, train)
     rows.append(y.numel() // y.shape[-1])
-    if _FUSED_STEM:  # BN+ReLU+maxpool, backward fused (ops.misc.BNReluPoolFn)
+    if _FUSED_STEM and not deterministic():  # BN+ReLU+maxpool, backward fused (ops.misc.BNReluPoolFn)
         y = BNReluPoolFn.apply(y, model.bn1, 3, 2, 1)
     else:
         y = _bn(y, model.bn1, True, train)

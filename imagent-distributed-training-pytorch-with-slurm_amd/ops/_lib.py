@@ -164,6 +164,8 @@ def _declare(name: str, lib) -> None:
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_eval_affine": [vp, i32, vp],
+            "imk_set_deterministic": [i32],
+            "imk_bn_stats_det": [vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, vp, i32, i32, i64, vp],
             "imk_bn_finalize_affine": [vp, vp, vp, vp, vp, vp, i32, i32, i64, f32, i32, vp],
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
@@ -195,6 +197,8 @@ def _declare(name: str, lib) -> None:
             f = getattr(lib, fn)
             f.argtypes = args
             f.restype = C.c_int
+        lib.imk_bn_stats_det_floats.argtypes = [i64, i32]
+        lib.imk_bn_stats_det_floats.restype = C.c_long
         # ABI guard: the ctypes mirrors must match the compiled structs
         for fn, st in [("imk_igemm_args_size", IGemmArgs), ("imk_wgrad_args_size", WgradArgs),
                        ("imk_bn_rundesc_size", RunDesc), ("imk_bn_affdesc_size", AffDesc), ("imk_tdesc_size", TDesc),

@@ -109,6 +109,37 @@ def set_stream(enabled: bool) -> None:
     _NOSTREAM = 0 if enabled else 2048
 
 
+# Deterministic mode (IMAGENT_DETERMINISTIC=1 or set_deterministic(True); bench / CLI --deterministic): BatchNorm
+# statistics without float atomics -- the forward statistics come from a fixed-order pass over the conv output
+# (bn.hip bn_stats_det_kernel) instead of the conv epilogue, and the backward reductions from the separate
+# reduce pass with a fixed-order fold (the models bind with bnb_fusion off and the unfused stem). Two passes over
+# the same data then give bit-identical statistics and activations; the weight gradients' split-K fp32 atomics
+# remain (order effects ~1e-7 relative, no feedback within a step).
+_DET = os.environ.get("IMAGENT_DETERMINISTIC", "0") == "1"
+
+
+def deterministic() -> bool:
+    return _DET
+
+
+_DET_LIB = None  # the mode last pushed to the kernel library
+
+
+def set_deterministic(on: bool) -> None:
+    """Switch the deterministic mode (before binding a model: it decides the BN-backward fusion)."""
+    global _DET, _DET_LIB
+    _DET = bool(on)
+    if torch.cuda.is_available():
+        _lib.check(_lib.kernels().imk_set_deterministic(1 if _DET else 0), "set deterministic")
+        _DET_LIB = _DET
+
+
+def _det_sync() -> None:
+    """The library follows this module's mode (e.g. IMAGENT_DETERMINISTIC=1 in a spawned worker)."""
+    if _DET_LIB != _DET:
+        set_deterministic(_DET)
+
+
 def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
               stats: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
@@ -159,13 +190,23 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     if xbn is not None:
         assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
         a.xbn = xbn.data_ptr()
+    det = None
     if stats is not None:
         if hasattr(stats, "slab"):  # a BatchNorm's workspace: shifted sums around its last batch mean
             if _SHIFT:
                 a.shift = stats.save.data_ptr()
             stats = stats.slab
-        a.stats = stats.data_ptr()
+        if _DET and not out_f32 and x.is_cuda:  # statistics by the fixed-order pass below
+            det, a.shift = (stats, a.shift), None
+        else:
+            a.stats = stats.data_ptr()
     _igemm_call(a, tile, _lib.stream_ptr(), "conv fwd")
+    if det is not None:
+        _det_sync()
+        k, R = _lib.kernels(), out.numel() // Co
+        part = torch.empty(k.imk_bn_stats_det_floats(R, Co), device=out.device, dtype=torch.float32)
+        _lib.check(k.imk_bn_stats_det(out.data_ptr(), det[1], det[0].data_ptr(), part.data_ptr(), R, Co,
+                                      _lib.stream_ptr()), "bn stats (deterministic)")
     return out
 
 

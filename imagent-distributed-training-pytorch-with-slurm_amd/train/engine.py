@@ -302,6 +302,9 @@ class Trainer:
             arena = self.native.arena
         elif self.kernels == "hip":
             from ..models.native import bind_native
+            if getattr(a, "deterministic", False):
+                from ..ops.conv import set_deterministic
+                set_deterministic(True)
             # IMAGENT_WGRAD_OVERLAP=0: weight gradients on the main stream (A/B and diagnostics)
             self.native = bind_native(model, self.device, order, fp8=a.dtype == "fp8",
                                       wgrad_overlap=os.environ.get("IMAGENT_WGRAD_OVERLAP", "1") != "0")

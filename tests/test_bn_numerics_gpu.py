@@ -78,3 +78,60 @@ def test_bn_fwd_relu_mask_bits(mode):
     torch.cuda.synchronize()
     assert (y > 0).any() and (y == 0).any()
     assert torch.equal(ym, relu_mask_bits(y))
+
+
+def test_deterministic_statistics():
+    """Deterministic mode: the conv's forward statistics come from the fixed-order pass over its output
+    (bn.hip bn_stats_det_kernel + det_fold_kernel): bit-identical across runs, equal to the epilogue
+    statistics and to fp64 over the stored bf16 output within fp32 rounding; the BN-backward reduce pass
+    with the fixed-order fold gives bit-identical dx / reductions across runs."""
+    from imagent_amd.models.resnet import BatchNorm2d
+    from imagent_amd.ops import conv as cv
+    from imagent_amd.ops.bn import bn_act_backward, stats_finalize
+    torch.manual_seed(5)
+    N, H, Ci, Co = 64, 28, 128, 256
+    x = torch.randn(N, H, H, Ci, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
+    shift = torch.randn(Co, device=DEV) * 0.1
+    prev = cv.deterministic()
+
+    def fwd(det):
+        work = _work(Co)
+        work.save[0].copy_(shift)
+        cv.set_deterministic(det)
+        try:
+            y = cv.igemm_fwd(x, w, 1, 1, 3, 3, stats=work)
+            stats_finalize(work, y.numel() // Co)
+        finally:
+            cv.set_deterministic(prev)
+        torch.cuda.synchronize()
+        return y, work.stats.clone()
+
+    y0, s0 = fwd(False)
+    y1, s1 = fwd(True)
+    y2, s2 = fwd(True)
+    assert torch.equal(y1, y2) and torch.equal(y0, y1)
+    assert torch.equal(s1, s2)
+    yd = y1.double().reshape(-1, Co)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    for s in (s0, s1):
+        assert ((s[0].double() - mean).abs() / (var.sqrt() + 1e-6)).max() < 1e-5
+        assert ((s[1].double() - var).abs() / var).max() < 1e-4
+    # backward reduce + apply, twice in the deterministic mode
+    bn = BatchNorm2d(Co).to(DEV)
+    bn.work = _work(Co)
+    bn.work.save.copy_(torch.stack([mean.float(), torch.rsqrt(var.float() + 1e-5)]))
+    bn.weight.grad = torch.zeros_like(bn.weight)
+    bn.bias.grad = torch.zeros_like(bn.bias)
+    g = torch.randn(N, H, H, Co, device=DEV).to(torch.bfloat16)
+    outs = []
+    cv.set_deterministic(True)
+    try:
+        for _ in range(2):
+            bn.work.scratch.zero_()
+            dx, _ = bn_act_backward(g, y1, None, None, bn, None, 0, True)
+            torch.cuda.synchronize()
+            outs.append((dx.clone(), bn.work.scratch.clone()))
+    finally:
+        cv.set_deterministic(prev)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
