@@ -26,7 +26,7 @@ import sqlite3
 
 PEAK_FLOPS = 2.5e15
 PEAK_BYTES = 8e12
-CONV_KERNELS = ("igemm_", "conv_stream_kernel", "halo3x3_kernel", "wgrad_kernel", "wgrad_v3_kernel")
+CONV_KERNELS = ("igemm_", "conv_stream_kernel", "halo3x3_kernel", "wgrad_")
 
 
 def flops_bytes(r):

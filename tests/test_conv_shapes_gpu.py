@@ -39,14 +39,17 @@ def _shapes(arch, size, batch):
 
 SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _shapes("resnet18", 448, 128)
 
-# conv kernel templates in the R50 bench trace (round 3, v15 trace: the v3 main loop in place of the
+# conv kernel templates in the R50 bench trace (round 3, v16 trace: the v3 main loop in place of the
 # igemm_dma 256x256 / 128x128 rings for C % 64 == 0); update together with the dispatcher
 BENCH_KERNELS = [
     "conv_stream_kernel<128, 128, 2, 0, false, true>",
+    "conv_stream_kernel<128, 128, 2, 1, false, false>",
+    "conv_stream_kernel<128, 128, 2, 3, false, false>",
     "conv_stream_kernel<224, 64, 2, 0, true, false>",
     "conv_stream_kernel<256, 64, 2, 0, false, false>",
     "conv_stream_kernel<256, 64, 2, 2, false, false>",
     "conv_stream_kernel<64, 128, 3, 1, false, false>",
+    "conv_stream_kernel<64, 128, 3, 3, false, false>",
     "conv_stream_kernel<64, 256, 3, 0, false, false>",
     "conv_stream_kernel<64, 256, 3, 0, false, true>",
     "conv_stream_kernel<64, 64, 3, 0, false, false>",
@@ -56,15 +59,15 @@ BENCH_KERNELS = [
     "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 128>",
     "igemm_v3_kernel<128, 128, 2, 2, 4, 128>",
     "igemm_v3_kernel<256, 256, 2, 2, 8, 128>",
+    "wgrad_halo_kernel<14, 14, 7, 16>",
+    "wgrad_halo_kernel<28, 4, 4, 32>",
+    "wgrad_halo_kernel<56, 4, 7, 64>",
     "wgrad_kernel<128, 128, 2, false, 4, 32, false, false>",
     "wgrad_kernel<128, 128, 2, false, 4, 32, false, true>",
     "wgrad_kernel<128, 128, 2, false, 4, 64, false, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false, false>",
     "wgrad_kernel<64, 128, 1, true, 4, 32, false, false>",
     "wgrad_v3_kernel<64, 2>",
-    "wgrad_halo_kernel<14, 14, 7, 16>",
-    "wgrad_halo_kernel<28, 4, 4, 32>",
-    "wgrad_halo_kernel<56, 4, 7, 64>",
 ]
 
 
