@@ -94,6 +94,9 @@ def main(argv=None):
     ap.add_argument("--eval", type=int, default=0,
                     help="N > 0: after the timed training steps, also time N validation steps (the folded-BN eval "
                          "forward + loss + top-k counters, imagenet.py:166-210) and report val_img_s")
+    ap.add_argument("--fp32-split", type=int, default=0,
+                    help="with --dtype fp32 --kernels hip: convs as 3 x bf16 split products (~2^-16 relative per "
+                         "product, within 1e-4 of fp32 convs) instead of the exact f32 MFMA")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="1: BatchNorm statistics without float atomics (fixed-order passes; ops/conv.py)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
@@ -167,6 +170,9 @@ def main(argv=None):
         if f32_hip:
             from imagent_amd.models.native_f32 import bind_native_f32
             native = bind_native_f32(model, dev, order)
+            if a.fp32_split:
+                from imagent_amd.ops.f32 import set_split
+                set_split(True)
             arena = native.arena
         elif a.kernels == "hip":
             from imagent_amd.models.native import bind_native
@@ -262,7 +268,8 @@ def main(argv=None):
                 "vs_baseline": round(value / base, 3) if base else None,
                 "dtype": ("fp32" if (not on_gpu or a.dtype == "fp32") else "bf16" if a.dtype == "bf16" else
                           "fp8 (e4m3 forward convs, bf16 backward)"),
-                "fp32_kernels": ("own exact-f32 MFMA kernels" if f32_hip else "PyTorch/MIOpen")
+                "fp32_kernels": (("own kernels: convs as 3 x bf16 split products (~2^-16 per product)"
+                                  if a.fp32_split else "own exact-f32 MFMA kernels") if f32_hip else "PyTorch/MIOpen")
                 if a.dtype == "fp32" else None,
                 "data": f"synthetic (uint8 3x{a.image_size}x{a.image_size} on device, GPU-normalised; "
                         "random-init weights)",

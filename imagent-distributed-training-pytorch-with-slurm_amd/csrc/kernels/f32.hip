@@ -169,6 +169,170 @@ __global__ __launch_bounds__(256, 2) void igemm_f32_kernel(const IGemmArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ conv fwd / dgrad, 3 x bf16 split
+// The same gather-GEMM with each fp32 operand split into bf16 hi + lo (x = hi + lo, |x - hi - lo| <= 2^-18 |x|)
+// and x*w computed as hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_bf16 (fp32 accumulate): the dropped lo*lo
+// term and the rounding of lo leave ~2^-16 relative per product, three bf16 MFMAs cost 3/16 of the f32 MFMA
+// cycles of the exact kernel above. Tile, loads and epilogue as igemm_f32_kernel; LDS per stage: hi / lo planes
+// of both operands as 64-B rows (32 k), 16-B chunk c of row r at slot c ^ ((r >> 2) & 3) (conflict-free
+// ds_read_b128 fragment reads: 16 rows of one chunk land on 16 distinct slots).
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void igemm_f32s_kernel(const IGemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int PLANE = F_BM * F_BK * 2;  // one [128][32] bf16 plane
+    constexpr int SBUF = 4 * PLANE;         // Xh, Xl, Wh, Wl
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wn = wid & 1, wm = wid >> 1;  // 2 x 2 waves, 64 x 64 each
+    const int nbn = (a.Nout + F_BN - 1) / F_BN;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    if (lid >= ((a.M + F_BM - 1) / F_BM) * nbn) return;
+    const int m0 = (lid / nbn) * F_BM, n0 = (lid % nbn) * F_BN;
+    const int K = a.nth * a.ntw * a.C;
+    const int nk = (K + F_BK - 1) / F_BK;
+    const int ohw = a.OH * a.OW;
+    const int col8 = tid & 7;  // this thread's 16-B fp32 chunk (4 k) of a staged row
+    const float* X = reinterpret_cast<const float*>(a.X);
+    const float* Wk = reinterpret_cast<const float*>(a.Wk);
+
+    const float* xrow[4];
+    int ih0[4], iw0[4];
+    bool mok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + (tid >> 3) + 32 * i;
+        mok[i] = m < a.M;
+        const int mm = mok[i] ? m : 0;
+        const int img = mm / ohw, rem = mm - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        xrow[i] = X + (size_t)img * a.H * a.W * a.C;
+        ih0[i] = oh * a.sA;
+        iw0[i] = ow * a.sA;
+    }
+    const float* wrow[4];
+    bool nok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = n0 + (tid >> 3) + 32 * j;
+        nok[j] = n < a.Nout;
+        wrow[j] = Wk + (size_t)(nok[j] ? n : 0) * a.ldb;
+    }
+    f32x4v rx[4], rw[4];
+    auto load = [&](int kt) {
+        const int k = kt * F_BK + col8 * 4;
+        int t, c;
+        if (MODE == 0) {
+            t = (kt * F_BK) / a.C;
+            c = kt * F_BK - t * a.C + col8 * 4;
+        } else {
+            t = k / a.C;
+            c = k - t * a.C;
+        }
+        const bool kok = k < K;
+        const int ti = kok ? t / a.ntw : 0, tj = kok ? t - ti * a.ntw : 0;
+        const int dh = a.dh0 + ti * a.dhs, dw = a.dw0 + tj * a.dws;
+        const int wtap = (a.kh0 + ti * a.khs) * a.KW + (a.kw0 + tj * a.kws);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ih = ih0[i] + dh, iw = iw0[i] + dw;
+            const bool ok = kok && mok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+            rx[i] = ok ? *reinterpret_cast<const f32x4v*>(xrow[i] + ((size_t)ih * a.W + iw) * a.C + c)
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            rw[j] = (kok && nok[j]) ? *reinterpret_cast<const f32x4v*>(wrow[j] + (size_t)wtap * a.C + c)
+                                    : f32x4v{0.f, 0.f, 0.f, 0.f};
+    };
+    // 4 fp32 -> 4 bf16 hi (8 B) + 4 bf16 lo (8 B) at row r, k = 4 col8 .. + 3
+    auto put = [&](char* hi_plane, char* lo_plane, int r, const f32x4v& v) {
+        const uint32_t h0 = pack_bf2(v[0], v[1]), h1 = pack_bf2(v[2], v[3]);
+        const uint32_t l0 = pack_bf2(v[0] - lo_bf(h0), v[1] - hi_bf(h0));
+        const uint32_t l1 = pack_bf2(v[2] - lo_bf(h1), v[3] - hi_bf(h1));
+        const int off = r * 64 + (((col8 >> 1) ^ ((r >> 2) & 3)) << 4) + ((col8 & 1) << 3);
+        *reinterpret_cast<u32x2*>(hi_plane + off) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(lo_plane + off) = u32x2{l0, l1};
+    };
+    auto store = [&](int buf) {
+        char* b = smem + buf * SBUF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = (tid >> 3) + 32 * i;
+            put(b, b + PLANE, r, rx[i]);
+            put(b + 2 * PLANE, b + 3 * PLANE, r, rw[i]);
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load(0);
+    store(0);
+    __syncthreads();
+    const int fr = lane & 15;
+    const int foff = fr * 64 + ((((lane >> 4) ^ ((fr >> 2) & 3))) << 4);  // row fr of a 16-row block, chunk lane>>4
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load(kt + 1);
+        const char* b = smem + buf * SBUF;
+        bf16x8 xh[4], xl[4], whi[4], wlo[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ro = (wn * 64 + i * 16) * 64 + foff;
+            whi[i] = *reinterpret_cast<const bf16x8*>(b + 2 * PLANE + ro);
+            wlo[i] = *reinterpret_cast<const bf16x8*>(b + 3 * PLANE + ro);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ro = (wm * 64 + j * 16) * 64 + foff;
+            xh[j] = *reinterpret_cast<const bf16x8*>(b + ro);
+            xl[j] = *reinterpret_cast<const bf16x8*>(b + PLANE + ro);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[i], xh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[i], xl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[i], xh[j], acc[i][j], 0, 0, 0);
+            }
+        if (kt + 1 < nk) {
+            __syncthreads();  // everyone is done reading buf ^ 1 (iteration kt - 1)
+            store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // epilogue: lane holds channels nb + i*16 + 4g + r of pixel mb + j*16 + fr (as igemm_f32_kernel)
+    const int g = lane >> 4;
+    const bool accum = a.flags & IG_ACCUM;
+    const float* bias = a.bias;
+    float* Y = reinterpret_cast<float*>(a.Y);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + fr;
+        if (m >= a.M) continue;
+        const int img = m / ohw, rem = m - img * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        float* yp = Y + (((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = n0 + wn * 64 + i * 16 + 4 * g;
+            f32x4 v = acc[i][j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (bias && n + r < a.Nout) v[r] += bias[n + r];
+            if (n + 3 < a.Nout && (a.ldy & 3) == 0) {
+                f32x4* p = reinterpret_cast<f32x4*>(yp + n);
+                if (accum) v += *p;
+                *p = v;
+            } else {
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < a.Nout) yp[n + r] = accum ? yp[n + r] + v[r] : v[r];
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ wgrad
 struct WgradF32Args {
     const float* dY;  // [M][Co] (output grid NHWC)
@@ -274,6 +438,155 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a)
         }
     }
     // lane: rows (co) co0 + wc*TCO + i*16 + 4g + r, column (k) k0 + wk*TK + j*16 + fr
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int k = k0 + wk * TK + j * 16 + fr;
+            if (k >= Kt) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + wc * TCO + i * 16 + 4 * g + r;
+                if (co < a.Co) atomicAdd(a.dW + (size_t)co * Kt + k, acc[i][j][r]);
+            }
+        }
+}
+
+// The weight gradient with the 3 x bf16 split (as igemm_f32s_kernel): a 32-pixel stage is one
+// v_mfma_f32_16x16x32_bf16 k-step; both operands staged as hi / lo bf16 planes of [32 px][256 B] rows
+// (chunk ch of row r at slot ch ^ (((r & 3) << 2) | ((r >> 2) & 3)), cdna_hip_programming.md T10 image (b);
+// a 64-column tile uses half of each row) and read as MFMA fragments by ds_read_b64_tr_b16 (pixels -> k),
+// the pixel order inside a fragment permuted identically for both operands (the sum over m does not care).
+__device__ __forceinline__ int wgs_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+template <int BCO, int BK>
+__global__ __launch_bounds__(256, 2) void wgrad_f32s_kernel(const WgradF32Args a) {
+    constexpr int WCO = BCO == 128 ? 2 : 1, WK = 4 / WCO;  // 4 waves
+    constexpr int TCO = BCO / WCO, TK = BK / WK;           // wave tile
+    constexpr int FI = TCO / 16, FJ = TK / 16;
+    constexpr int CA = WG_M * BCO / 4 / 256, CB = WG_M * BK / 4 / 256;  // fp32 16-B chunks per thread per stage
+    constexpr int PL = WG_M * 256;                                      // one bf16 plane, bytes
+    extern __shared__ __attribute__((aligned(16))) char smem[];          // [2][Ah, Al, Bh, Bl]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wc = wid % WCO, wk = wid / WCO;
+    const int Kt = a.KH * a.KW * a.C;
+    const int nco = (a.Co + BCO - 1) / BCO, nkt = (Kt + BK - 1) / BK;
+    const int tile = blockIdx.x % (nco * nkt), split = blockIdx.x / (nco * nkt);
+    const int co0 = (tile % nco) * BCO, k0 = (tile / nco) * BK;
+    const int mbeg = split * a.m_per_split, mend = min(a.M, mbeg + a.m_per_split);
+    if (mbeg >= mend) return;
+    const int ohw = a.OH * a.OW;
+    f32x4v ra[CA], rb[CB];
+    auto load = [&](int mb) {
+#pragma unroll
+        for (int u = 0; u < CA; ++u) {
+            const int q = tid + 256 * u;
+            const int r = q / (BCO / 4), cc = (q % (BCO / 4)) * 4;
+            const int m = mb + r, co = co0 + cc;
+            ra[u] = (m < mend && co < a.Co) ? *reinterpret_cast<const f32x4v*>(a.dY + (size_t)m * a.Co + co)
+                                            : f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int q = tid + 256 * u;
+            const int r = q / (BK / 4), kc = (q % (BK / 4)) * 4;
+            const int m = mb + r, k = k0 + kc;
+            f32x4v v = {0.f, 0.f, 0.f, 0.f};
+            if (m < mend && k < Kt) {
+                const int t = k / a.C, c = k - t * a.C;
+                const int kh = t / a.KW, kw = t - kh * a.KW;
+                const int img = m / ohw, rem = m - img * ohw;
+                const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                    v = *reinterpret_cast<const f32x4v*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.C + c);
+            }
+            rb[u] = v;
+        }
+    };
+    // 4 fp32 at (row r, column col .. col + 3) -> 8 B of the hi plane + 8 B of the lo plane
+    auto put = [&](char* hp, char* lp, int r, int col, const f32x4v& v) {
+        const uint32_t h0 = pack_bf2(v[0], v[1]), h1 = pack_bf2(v[2], v[3]);
+        const uint32_t l0 = pack_bf2(v[0] - lo_bf(h0), v[1] - hi_bf(h0));
+        const uint32_t l1 = pack_bf2(v[2] - lo_bf(h1), v[3] - hi_bf(h1));
+        const int off = r * 256 + (((col >> 3) ^ wgs_swz(r)) << 4) + ((col & 4) << 1);
+        *reinterpret_cast<u32x2*>(hp + off) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(lp + off) = u32x2{l0, l1};
+    };
+    auto store = [&](int buf) {
+        char* b = smem + buf * 4 * PL;
+#pragma unroll
+        for (int u = 0; u < CA; ++u) {
+            const int q = tid + 256 * u;
+            put(b, b + PL, q / (BCO / 4), (q % (BCO / 4)) * 4, ra[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int q = tid + 256 * u;
+            put(b + 2 * PL, b + 3 * PL, q / (BK / 4), (q % (BK / 4)) * 4, rb[u]);
+        }
+    };
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // transposed-read addressing (as wgrad_v3_kernel): group g reads rows r1 + q and r1 + 16 + q
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int r1 = (g & 1) * 8 + (g >> 1) * 4 + q4, r2 = r1 + 16;
+    int offa[FI][2], offb[FJ][2];
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+        const int ca = (wc * TCO) / 8 + 2 * i + (p4 >> 1);
+        offa[i][0] = r1 * 256 + ((ca ^ wgs_swz(r1)) << 4) + 8 * (p4 & 1);
+        offa[i][1] = r2 * 256 + ((ca ^ wgs_swz(r2)) << 4) + 8 * (p4 & 1);
+    }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+        const int cb = (wk * TK) / 8 + 2 * j + (p4 >> 1);
+        offb[j][0] = r1 * 256 + ((cb ^ wgs_swz(r1)) << 4) + 8 * (p4 & 1);
+        offb[j][1] = r2 * 256 + ((cb ^ wgs_swz(r2)) << 4) + 8 * (p4 & 1);
+    }
+    auto frag = [&](const char* plane, const int (&o)[2]) {
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(plane + o[0]));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(s16x4))(plane + o[1]));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    const int nst = (mend - mbeg + WG_M - 1) / WG_M;
+    load(mbeg);
+    store(0);
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nst) load(mbeg + (s + 1) * WG_M);
+        const char* b = smem + buf * 4 * PL;
+        bf16x8 ah[FI], al[FI], bh[FJ], bl[FJ];
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            ah[i] = frag(b, offa[i]);
+            al[i] = frag(b + PL, offa[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            bh[j] = frag(b + 2 * PL, offb[j]);
+            bl[j] = frag(b + 3 * PL, offb[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+        if (s + 1 < nst) {
+            __syncthreads();
+            store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // lane: rows (co) co0 + wc*TCO + i*16 + 4g + r, column (k) k0 + wk*TK + j*16 + (lane & 15)
+    const int fr = lane & 15;
 #pragma unroll
     for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -592,13 +905,29 @@ int bn_blocks(long R, int C) {
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
+// fp32 conv arithmetic: 0 exact f32 MFMA (igemm_f32_kernel, wgrad_f32_kernel), 1 the 3 x bf16 split
+// (igemm_f32s_kernel, wgrad_f32s_kernel)
+static int g_f32_split = [] {
+    const char* e = getenv("IMAGENT_F32_SPLIT");
+    return e ? atoi(e) : 0;
+}();
+IMK_EXPORT int imk_set_f32_split(int on) {
+    g_f32_split = on ? 1 : 0;
+    return 0;
+}
+
 IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
     const IGemmArgs& a = *args;
     if (a.M <= 0 || a.Nout <= 0) return 0;
     if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32))) return -100;
     const int ntiles = ((a.M + F_BM - 1) / F_BM) * ((a.Nout + F_BN - 1) / F_BN);
-    const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);
-    if (a.C % F_BK == 0)
+    const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);  // (= the split kernel's 2 x 4 bf16 planes)
+    if (g_f32_split) {
+        if (a.C % F_BK == 0)
+            hipLaunchKernelGGL(igemm_f32s_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL(igemm_f32s_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+    } else if (a.C % F_BK == 0)
         hipLaunchKernelGGL(igemm_f32_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(igemm_f32_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
@@ -620,6 +949,16 @@ IMK_EXPORT int imk_wgrad_f32(const float* dy, const float* x, float* dw, int N, 
     splits = std::max(1, std::min(splits, max_splits));
     a.m_per_split = ((a.M + splits - 1) / splits + WG_M - 1) / WG_M * WG_M;
     splits = (a.M + a.m_per_split - 1) / a.m_per_split;
+    if (g_f32_split) {  // 3 x bf16 split: hi / lo planes of [32 px][256 B], two buffers
+        const size_t lds = 2 * 4 * WG_M * 256;
+        if (small)
+            hipLaunchKernelGGL((wgrad_f32s_kernel<64, 128>), dim3(tiles * splits), dim3(256), lds, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL((wgrad_f32s_kernel<128, 128>), dim3(tiles * splits), dim3(256), lds, (hipStream_t)stream,
+                               a);
+        IMK_CHECK_LAUNCH();
+        return 0;
+    }
     const size_t lds = 2 * 2 * WG_M * WG_P * sizeof(float);
     if (small)
         hipLaunchKernelGGL((wgrad_f32_kernel<64, 128>), dim3(tiles * splits), dim3(256), lds, (hipStream_t)stream, a);

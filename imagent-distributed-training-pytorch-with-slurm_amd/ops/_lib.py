@@ -146,6 +146,7 @@ def _declare(name: str, lib) -> None:
             "imk_conv_launches": [],
             # fp32 path (f32.hip)
             "imk_conv_f32": [C.POINTER(IGemmArgs), vp],
+            "imk_set_f32_split": [i32],
             "imk_wgrad_f32": [vp, vp, vp] + [i32] * 11 + [vp],
             "imk_bn_slab_floats_f32": [i32],
             "imk_bn_stats_f32": [vp, vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],

@@ -26,6 +26,13 @@ def _k():
 
 
 # ------------------------------------------------------------------ convolution
+def set_split(on: bool) -> None:
+    """fp32 conv (forward / dgrad / wgrad) arithmetic: False (default) exact f32 MFMA; True the 3 x bf16 split
+    (hi*hi + hi*lo + lo*hi on the bf16 MFMA, ~2^-16 relative per product, within 1e-4 of fp32 convs;
+    f32.hip igemm_f32s_kernel / wgrad_f32s_kernel; bench.py --fp32-split)."""
+    _lib.check(_k().imk_set_f32_split(1 if on else 0), "set f32 split")
+
+
 def conv_f32(x: torch.Tensor, wk: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
              bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
              accumulate: bool = False) -> torch.Tensor:

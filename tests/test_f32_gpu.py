@@ -70,6 +70,35 @@ def test_conv_f32_fwd_dgrad_wgrad(shape):
     assert as_good(dw.permute(0, 3, 1, 2), w.grad, w64.grad)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (3, 72, 11, 200, 3, 2, 1), (2, 256, 9, 512, 1, 1, 0),
+                                   (3, 4, 38, 64, 7, 2, 3), (2, 64, 57, 64, 3, 1, 1), (5, 96, 7, 40, 1, 1, 0)])
+def test_conv_f32_split(shape):
+    """The 3 x bf16 split forward / dgrad / wgrad (f32.hip igemm_f32s_kernel, wgrad_f32s_kernel,
+    ops.f32.set_split): within 1e-4 of the PyTorch fp32 conv (normwise) -- ~2^-16 per product, not the exact
+    kernels' as-good-as-fp32 bound."""
+    from imagent_amd.ops.f32 import conv_f32, dgrad_f32, set_split, wgrad_f32
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, Ci, H, H, device=DEV, requires_grad=True)
+    w = (torch.randn(Co, Ci, k, k, device=DEV) * (2.0 / (Ci * k * k)) ** 0.5).requires_grad_(True)
+    y = F.conv2d(x, w, None, s, p)
+    g = torch.randn_like(y)
+    y.backward(g)
+    wk = w.detach().permute(0, 2, 3, 1).contiguous()
+    set_split(True)
+    try:
+        got = conv_f32(nhwc(x.detach()), wk, s, p, k, k)
+        dx = dgrad_f32(nhwc(g), wk.permute(3, 1, 2, 0).contiguous(), (H, H), s, p, k, k)
+        dw = torch.zeros(Co, k, k, Ci, device=DEV)
+        wgrad_f32(nhwc(g), nhwc(x.detach()), dw, s, p, k, k)
+        torch.cuda.synchronize()
+    finally:
+        set_split(False)
+    assert rel(nchw(got), y) < TOL, rel(nchw(got), y)
+    assert rel(nchw(dx), x.grad) < TOL, rel(nchw(dx), x.grad)
+    assert rel(dw.permute(0, 3, 1, 2), w.grad) < TOL, rel(dw.permute(0, 3, 1, 2), w.grad)
+
+
 @pytest.mark.parametrize("C,res,relu", [(64, False, True), (128, True, True), (256, False, False), (512, True, True)])
 def test_bn_f32(C, res, relu):
     from imagent_amd.models.resnet import BatchNorm2d
