@@ -133,8 +133,7 @@ __global__ __launch_bounds__(256, 2) void igemm_f32_kernel(const IGemmArgs a) {
                     for (int j = 0; j < 4; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fw[i][s], fx[j][s], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) {
-            __syncthreads();  // everyone is done reading buf ^ 1 (iteration kt - 1)
+        if (kt + 1 < nk) {  // buf ^ 1 was last read in iteration kt - 1, before its closing barrier
             store(buf ^ 1);
             __syncthreads();
         }
@@ -296,8 +295,7 @@ __global__ __launch_bounds__(256, 2) void igemm_f32s_kernel(const IGemmArgs a) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[i], xl[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[i], xh[j], acc[i][j], 0, 0, 0);
             }
-        if (kt + 1 < nk) {
-            __syncthreads();  // everyone is done reading buf ^ 1 (iteration kt - 1)
+        if (kt + 1 < nk) {  // buf ^ 1 was last read in iteration kt - 1, before its closing barrier
             store(buf ^ 1);
             __syncthreads();
         }
@@ -344,6 +342,43 @@ struct WgradF32Args {
 constexpr int WG_M = 32;      // pixels per stage
 constexpr int WG_P = 144;     // LDS row pitch (floats)
 
+// The im2col gather of one 16-B chunk per (thread, u) of the wgrad X operand: its k column (tap kh, kw and
+// channel c) never changes and its pixel row moves by exactly WG_M per stage, so the tap is decoded once and
+// the pixel (img, oh, ow) is a cursor stepped by WG_M (no integer divisions in the main loop).
+struct WgGather {
+    int kh, kw, c, m, img, oh, ow;
+    __device__ void init(const WgradF32Args& a, int k, int m0, int Kt) {
+        const int kk = k < Kt ? k : 0;
+        const int t = kk / a.C;
+        c = kk - t * a.C;
+        kh = k < Kt ? t / a.KW : -(1 << 20);  // a column past Kt never hits the image
+        kw = t - (t / a.KW) * a.KW;
+        m = m0;
+        const int ohw = a.OH * a.OW;
+        img = m0 / ohw;
+        const int rem = m0 - img * ohw;
+        oh = rem / a.OW;
+        ow = rem - oh * a.OW;
+    }
+    __device__ f32x4v load(const WgradF32Args& a, int mend) const {
+        const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+        if (m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+            return *reinterpret_cast<const f32x4v*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.C + c);
+        return f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ void step(const WgradF32Args& a) {
+        m += WG_M;
+        ow += WG_M;
+        while (ow >= a.OW) {
+            ow -= a.OW;
+            if (++oh == a.OH) {
+                oh = 0;
+                ++img;
+            }
+        }
+    }
+};
+
 template <int BCO, int BK>
 __global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a) {
     constexpr int WCO = BCO == 128 ? 2 : 1, WK = 4 / WCO;  // 4 waves
@@ -361,7 +396,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a)
     const int co0 = (tile % nco) * BCO, k0 = (tile / nco) * BK;
     const int mbeg = split * a.m_per_split, mend = min(a.M, mbeg + a.m_per_split);
     if (mbeg >= mend) return;
-    const int ohw = a.OH * a.OW;
+    WgGather gb[CB];
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+        const int q = tid + 256 * u;
+        gb[u].init(a, k0 + (q % (BK / 4)) * 4, mbeg + q / (BK / 4), Kt);
+    }
     // chunk assignment: A chunk q -> (row = q / (BCO/4), col4 = q % (BCO/4)); same for B with BK
     f32x4v ra[CA], rb[CB];
     auto load = [&](int mb) {
@@ -375,20 +415,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a)
         }
 #pragma unroll
         for (int u = 0; u < CB; ++u) {
-            const int q = tid + 256 * u;
-            const int r = q / (BK / 4), kc = (q % (BK / 4)) * 4;
-            const int m = mb + r, k = k0 + kc;
-            f32x4v v = {0.f, 0.f, 0.f, 0.f};
-            if (m < mend && k < Kt) {
-                const int t = k / a.C, c = k - t * a.C;
-                const int kh = t / a.KW, kw = t - kh * a.KW;
-                const int img = m / ohw, rem = m - img * ohw;
-                const int oh = rem / a.OW, ow = rem - oh * a.OW;
-                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                    v = *reinterpret_cast<const f32x4v*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.C + c);
-            }
-            rb[u] = v;
+            rb[u] = gb[u].load(a, mend);
+            gb[u].step(a);
         }
     };
     auto store = [&](int buf) {
@@ -431,8 +459,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_kernel(const WgradF32Args a)
                 for (int j = 0; j < FJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
-        if (s + 1 < nst) {
-            __syncthreads();
+        if (s + 1 < nst) {  // buf ^ 1 was last read in stage s - 1, before its closing barrier
             store(buf ^ 1);
             __syncthreads();
         }
@@ -475,7 +502,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32s_kernel(const WgradF32Args a
     const int co0 = (tile % nco) * BCO, k0 = (tile / nco) * BK;
     const int mbeg = split * a.m_per_split, mend = min(a.M, mbeg + a.m_per_split);
     if (mbeg >= mend) return;
-    const int ohw = a.OH * a.OW;
+    WgGather gb[CB];
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+        const int q = tid + 256 * u;
+        gb[u].init(a, k0 + (q % (BK / 4)) * 4, mbeg + q / (BK / 4), Kt);
+    }
     f32x4v ra[CA], rb[CB];
     auto load = [&](int mb) {
 #pragma unroll
@@ -488,20 +520,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32s_kernel(const WgradF32Args a
         }
 #pragma unroll
         for (int u = 0; u < CB; ++u) {
-            const int q = tid + 256 * u;
-            const int r = q / (BK / 4), kc = (q % (BK / 4)) * 4;
-            const int m = mb + r, k = k0 + kc;
-            f32x4v v = {0.f, 0.f, 0.f, 0.f};
-            if (m < mend && k < Kt) {
-                const int t = k / a.C, c = k - t * a.C;
-                const int kh = t / a.KW, kw = t - kh * a.KW;
-                const int img = m / ohw, rem = m - img * ohw;
-                const int oh = rem / a.OW, ow = rem - oh * a.OW;
-                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-                if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                    v = *reinterpret_cast<const f32x4v*>(a.X + (((size_t)img * a.H + ih) * a.W + iw) * a.C + c);
-            }
-            rb[u] = v;
+            rb[u] = gb[u].load(a, mend);
+            gb[u].step(a);
         }
     };
     // 4 fp32 at (row r, column col .. col + 3) -> 8 B of the hi plane + 8 B of the lo plane
@@ -579,8 +599,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32s_kernel(const WgradF32Args a
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
             }
-        if (s + 1 < nst) {
-            __syncthreads();
+        if (s + 1 < nst) {  // buf ^ 1 was last read in stage s - 1, before its closing barrier
             store(buf ^ 1);
             __syncthreads();
         }

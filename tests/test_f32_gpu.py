@@ -173,7 +173,8 @@ def test_pool_fc_xent_f32():
     assert rel(z.grad, zr.grad) < TOL
 
 
-def test_resnet18_f32_training_step_matches_torch():
+@pytest.mark.parametrize("split", [False, True])
+def test_resnet18_f32_training_step_matches_torch(split):
     """Two full training steps (normalise -> forward -> xent -> backward -> SGD) of ResNet-18 on the
     fp32 kernels against the same model in float64 (PyTorch ops). The first forward (loss) is within
     1e-4 relative; what depends on the gradients (updated parameters, the second loss, eval logits)
@@ -185,7 +186,23 @@ def test_resnet18_f32_training_step_matches_torch():
     every gradient below it by as much (scripts/f32_diag.py: one flip at layer3.1.bn1 gives exactly
     the 1-3e-3 seen at every earlier layer, with the same gradients computed under float64's mask
     matching to 2.5e-6; PyTorch fp32 flips too on other seeds, 4.5e-3 at layer1.1.bn2.bias).
+    ``split``: every conv on the 3 x bf16 split kernels (bench.py --fp32-split). ~2^-16 per product puts
+    ~10x more activations within rounding of the ReLU threshold, so the flip-driven gradient floor is
+    4e-2 (measured 1.0-1.5e-2 at the first layers) -- still tighter than the TF32 convs PyTorch runs
+    fp32 models on by default on the reference's GPUs (10-bit mantissa, 2^-11 per product). The oracles
+    restart step 2 from OUR weights: after the lr-0.1 step on 8 images (loss 4.74 -> 2.75) the step-2
+    gradients amplify a 1e-2 step-1 gradient difference ~40x (measured 0.4 against oracles that kept
+    their own weights, with the step-2 loss still within 2e-3).
     """
+    from imagent_amd.ops.f32 import set_split
+    set_split(split)
+    try:
+        _r18_f32_steps(4e-2 if split else 1e-2, split)
+    finally:
+        set_split(False)
+
+
+def _r18_f32_steps(gfloor, resync):
     import copy
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.models import resnet
@@ -214,6 +231,14 @@ def test_resnet18_f32_training_step_matches_torch():
         return rel(ours, exact) <= max(3 * rel(oracle32, exact), floor)
 
     for it in range(2):
+        if resync and it:  # weights, BN statistics and momentum buffers from ours
+            for mm in (ref, ref64):
+                mm.load_state_dict(m.state_dict())
+            ours, ra, p64 = st.arena, models[0][1], dict(ref64.named_parameters())
+            for i, n in enumerate(ours.names):
+                b = ours.view(opts[2].buf, i)
+                ra.view(opts[0].buf, ra.names.index(n)).copy_(b)
+                opts[1].state[p64[n]]["momentum_buffer"].copy_(b)
         for mm, _ in models:
             mm.train()
         for o in opts:
@@ -232,15 +257,18 @@ def test_resnet18_f32_training_step_matches_torch():
         g32 = {n: p.grad for n, p in ref.named_parameters()}
         g64 = {n: p.grad for n, p in ref64.named_parameters()}
         bad = [(n, f"{rel(p.grad, g64[n]):.2e}", f"{rel(g32[n], g64[n]):.2e}") for n, p in m.named_parameters()
-               if not close(p.grad, g32[n], g64[n], 1e-2)]
+               if not close(p.grad, g32[n], g64[n], gfloor)]
         assert not bad, (it, bad)
         for o in opts:
             o.step()
+    # split: a parameter made of its updates (BatchNorm biases start at 0) inherits the step-2 gradient
+    # difference (measured 6.4e-3 at layer1.0.bn1.bias)
+    sfloor = 1e-2 if resync else 2e-3
     sd32, sd64 = ref.state_dict(), ref64.state_dict()
     for n, a in m.state_dict().items():
         if a.dtype.is_floating_point:
-            assert close(a, sd32[n], sd64[n], 2e-3), n
+            assert close(a, sd32[n], sd64[n], sfloor), (n, rel(a, sd64[n]))
     for mm, _ in models:
         mm.eval()
     with torch.no_grad():
-        assert close(m(xh), ref(xr), ref64(xr.double()), 2e-3)
+        assert close(m(xh), ref(xr), ref64(xr.double()), sfloor), rel(m(xh), ref64(xr.double()))
