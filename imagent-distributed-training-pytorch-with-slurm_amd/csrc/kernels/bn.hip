@@ -274,12 +274,25 @@ __global__ __launch_bounds__(256) void bn_stats_det_kernel(const bf16_t* __restr
 }
 
 // out[i] += sum over b = 0 .. nb - 1 (in that order) of partial[b * stride + i], i < n
-__global__ void det_fold_kernel(const float* __restrict__ partial, int nb, int stride, int n, float* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// 16 columns per 256-thread block, 16 fixed row partitions per column (rows b = part, part + 16, ...) summed
+// in order, then the 16 partition sums in order: deterministic, and 16 independent load streams per column
+// instead of one serial walk over up to 1024 rows
+constexpr int DET_COLS = 16;
+__global__ __launch_bounds__(256) void det_fold_kernel(const float* __restrict__ partial, int nb, int stride, int n,
+                                                       float* __restrict__ out) {
+    __shared__ float red[16][DET_COLS];
+    const int cl = threadIdx.x % DET_COLS, part = threadIdx.x / DET_COLS;
+    const int i = blockIdx.x * DET_COLS + cl;
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += partial[(size_t)b * stride + i];
-    out[i] += s;
+    if (i < n)
+        for (int b = part; b < nb; b += 16) s += partial[(size_t)b * stride + i];
+    red[part][cl] = s;
+    __syncthreads();
+    if (part || i >= n) return;
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][cl];
+    out[i] += t;
 }
 
 int g_det = 0;            // deterministic mode (imk_set_deterministic)
@@ -808,7 +821,7 @@ IMK_EXPORT int imk_bn_stats_det(const void* y, const float* shift, float* slab, 
     const int grid = std::min(grid_for(R, C), 2048);
     hipLaunchKernelGGL(bn_stats_det_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)y, shift, partial, R, C);
     IMK_CHECK_LAUNCH();
-    hipLaunchKernelGGL(det_fold_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, partial, grid, 2 * C, 2 * C,
+    hipLaunchKernelGGL(det_fold_kernel, dim3((2 * C + DET_COLS - 1) / DET_COLS), dim3(256), 0, st, partial, grid, 2 * C, 2 * C,
                        slab);
     IMK_CHECK_LAUNCH();
     return 0;
@@ -858,7 +871,7 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     IMK_CHECK_LAUNCH();
     if (det) {  // the blocks' rows in block order into slot 0
         const int n = (mode == 2 ? 3 : 2) * C;  // the quantities this mode reduces
-        hipLaunchKernelGGL(det_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, st, det, rgrid, 3 * C, n, scratch);
+        hipLaunchKernelGGL(det_fold_kernel, dim3((n + DET_COLS - 1) / DET_COLS), dim3(256), 0, st, det, rgrid, 3 * C, n, scratch);
         IMK_CHECK_LAUNCH();
     }
     float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
