@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256) void det_fold_kernel(const float* __restrict__
     const int i = blockIdx.x * DET_COLS + cl;
     float s = 0.f;
     if (i < n)
-        for (int b = part; b < nb; b += 16) s += partial[(size_t)b * stride + i];
+#pragma unroll 8
+        for (int b = part; b < nb; b += 16) s += partial[(size_t)b * stride + i];  // loads batched, adds in order
     red[part][cl] = s;
     __syncthreads();
     if (part || i >= n) return;

@@ -693,7 +693,8 @@ __device__ __forceinline__ void fold_slab(const float* __restrict__ slab, int nb
     active = c < C;
     double s1 = 0.0, s2 = 0.0;
     if (active)
-        for (int b = part; b < nb; b += 16) {
+#pragma unroll 8
+        for (int b = part; b < nb; b += 16) {  // loads batched, adds in order
             s1 += slab[((size_t)b * 2) * C + c];
             s2 += slab[((size_t)b * 2 + 1) * C + c];
         }
