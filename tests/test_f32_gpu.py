@@ -189,15 +189,18 @@ def test_resnet18_f32_training_step_matches_torch(split):
     ``split``: every conv on the 3 x bf16 split kernels (bench.py --fp32-split). ~2^-16 per product puts
     ~10x more activations within rounding of the ReLU threshold, so the flip-driven gradient floor is
     4e-2 (measured 1.0-1.5e-2 at the first layers) -- still tighter than the TF32 convs PyTorch runs
-    fp32 models on by default on the reference's GPUs (10-bit mantissa, 2^-11 per product). The oracles
-    restart step 2 from OUR weights: after the lr-0.1 step on 8 images (loss 4.74 -> 2.75) the step-2
-    gradients amplify a 1e-2 step-1 gradient difference ~40x (measured 0.4 against oracles that kept
-    their own weights, with the step-2 loss still within 2e-3).
+    fp32 models on by default on the reference's GPUs (10-bit mantissa, 2^-11 per product).
+
+    In both modes the oracles restart step 2 from OUR state (weights, BatchNorm statistics, momentum): after
+    the lr-0.1 step on 8 images (loss 4.74 -> 2.75) the step-2 gradients amplify a step-1 gradient difference
+    ~40-100x (measured: split 1e-2 -> 0.4; exact, on a run where one ReLU flip gave 2e-3, -> 0.2, with
+    PyTorch fp32's own step-1 flip at 2.3e-3), so oracles that kept their own weights test the chaos, not
+    the kernels.
     """
     from imagent_amd.ops.f32 import set_split
     set_split(split)
     try:
-        _r18_f32_steps(4e-2 if split else 1e-2, split)
+        _r18_f32_steps(4e-2 if split else 1e-2, True)
     finally:
         set_split(False)
 
@@ -261,9 +264,9 @@ def _r18_f32_steps(gfloor, resync):
         assert not bad, (it, bad)
         for o in opts:
             o.step()
-    # split: a parameter made of its updates (BatchNorm biases start at 0) inherits the step-2 gradient
-    # difference (measured 6.4e-3 at layer1.0.bn1.bias)
-    sfloor = 1e-2 if resync else 2e-3
+    # a parameter made of its updates (BatchNorm biases start at 0) inherits the step-2 gradient difference
+    # (split: measured 6.4e-3 at layer1.0.bn1.bias)
+    sfloor = 1e-2 if gfloor > 1e-2 else 2e-3
     sd32, sd64 = ref.state_dict(), ref64.state_dict()
     for n, a in m.state_dict().items():
         if a.dtype.is_floating_point:

@@ -52,6 +52,10 @@ def _curve(out):
 # early loss spike whose size and timing are chaotic (profiles/convergence_r50.md), e.g. an oracle run
 # measured at 2.00 / 0.46 epoch means against the HIP run's 0.49 / 0.002
 WARM = ["--warmup-epochs", "0.5"]
+# the variant / A-B-switch tests only ask "does it learn": at lr 0.05 a run can still leave the basin after
+# it has learned the task (measured: accum2 epoch means 0.65 -> 1.59; IMAGENT_BN_SHIFT=0 1.47 -> 3.79 over
+# 40 iterations, both passing on other runs of the same build), so they train at a calmer lr
+CALM = ["--lr", "0.02"]
 
 
 def test_hip_training_converges_saves_and_resumes(tmp_path):
@@ -83,7 +87,7 @@ def test_hip_training_converges_saves_and_resumes(tmp_path):
 
 @pytest.mark.parametrize("extra", [["--accum-steps", "2"], ["--dtype", "fp8"]], ids=["accum2", "fp8"])
 def test_hip_training_variants_converge(tmp_path, extra):
-    out = _run(BASE + WARM + ["--kernels", "hip", "--epochs", "2"] + extra, tmp_path)
+    out = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "2"] + extra, tmp_path)
     first, summ, top1 = _curve(out)
     assert len(top1) == 2, out[-3000:]
     # epoch-2 mean under a third of the chance-level loss ln 10 (the first logged interval is no
@@ -97,7 +101,7 @@ def test_bn_shift_off_switch_trains(tmp_path):
     add the previous batch mean back (it did: NaN losses from the second step on)."""
     # (with half an epoch of LR warmup, as the other trainer tests: without it an early run can pass through
     # a chaotic phase -- one measured 1.12 -> 1.71 -> 1.45 -> 2.41 over the epoch's logged intervals)
-    out = _run(BASE + WARM + ["--kernels", "hip", "--epochs", "1", "--synthetic-train-size", str(32 * 40)],
+    out = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "1", "--synthetic-train-size", str(32 * 40)],
                tmp_path, IMAGENT_BN_SHIFT="0")
     first, summ, top1 = _curve(out)
     assert len(summ) == 1 and all(v == v for v in first) and summ[0][0] == summ[0][0], out[-2000:]
