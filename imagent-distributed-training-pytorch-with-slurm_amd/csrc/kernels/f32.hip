@@ -748,21 +748,32 @@ __global__ __launch_bounds__(256) void bn_fold_bwd_f32_kernel(const float* __res
     if (dgamma) dgamma[c] += (float)a2;
 }
 
-// y = (x - mean) rstd gamma + beta (+ res) (ReLU)
+// y = (x - mean) rstd gamma + beta (+ res) (ReLU). FIXED: the grid stride (gridDim * 1024 elements) is a
+// multiple of C, so a thread's 4 channels never change and their coefficients are loaded once
+template <bool FIXED>
 __global__ __launch_bounds__(256) void bn_apply_f32_kernel(const float* __restrict__ x, const float* __restrict__ save,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
                                                            const float* __restrict__ res, float* __restrict__ y,
                                                            long n4, int C, int relu) {
-    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < n4; t += (long)gridDim.x * 256) {
-        const int c0 = (int)((t * 4) % C);
-        const f32x4v xv = reinterpret_cast<const f32x4v*>(x)[t];
-        f32x4v o;
+    const long t0 = (long)blockIdx.x * 256 + threadIdx.x;
+    float mean[4], sc[4], sh[4];
+    auto coef = [&](int c0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int c = c0 + q;
-            o[q] = (xv[q] - save[c]) * save[C + c] * gamma[c] + beta[c];
+            mean[q] = save[c];
+            sc[q] = save[C + c] * gamma[c];
+            sh[q] = beta[c];
         }
+    };
+    if (FIXED) coef((int)((t0 * 4) % C));
+    for (long t = t0; t < n4; t += (long)gridDim.x * 256) {
+        if (!FIXED) coef((int)((t * 4) % C));
+        const f32x4v xv = reinterpret_cast<const f32x4v*>(x)[t];
+        f32x4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (xv[q] - mean[q]) * sc[q] + sh[q];
         if (res) o += reinterpret_cast<const f32x4v*>(res)[t];
         if (relu)
 #pragma unroll
@@ -772,6 +783,7 @@ __global__ __launch_bounds__(256) void bn_apply_f32_kernel(const float* __restri
 }
 
 // dx = gamma rstd (g' - sum(g')/R - xhat sum(g' xhat)/R); dres = g' (when requested)
+template <bool FIXED>  // as bn_apply_f32_kernel
 __global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __restrict__ g,
                                                                const float* __restrict__ y,
                                                                const float* __restrict__ x,
@@ -779,8 +791,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __re
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ red, float* __restrict__ dx,
                                                                float* __restrict__ dres, long n4, int C, float inv) {
-    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < n4; t += (long)gridDim.x * 256) {
-        const int c0 = (int)((t * 4) % C);
+    const long t0 = (long)blockIdx.x * 256 + threadIdx.x;
+    // dx = gamma rstd (g' - sum(g')/R - (x - mean) rstd sum(g' xhat)/R)
+    float mean[4], k1[4], r0[4], r1[4];
+    auto coef = [&](int c0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = c0 + q;
+            const float rstd = save[C + c];
+            mean[q] = save[c];
+            k1[q] = gamma[c] * rstd;
+            r0[q] = red[c] * inv;
+            r1[q] = rstd * (red[C + c] * inv);
+        }
+    };
+    if (FIXED) coef((int)((t0 * 4) % C));
+    for (long t = t0; t < n4; t += (long)gridDim.x * 256) {
+        if (!FIXED) coef((int)((t * 4) % C));
         f32x4v gv = reinterpret_cast<const f32x4v*>(g)[t];
         if (y) {
             const f32x4v yv = reinterpret_cast<const f32x4v*>(y)[t];
@@ -792,12 +819,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __re
         const f32x4v xv = reinterpret_cast<const f32x4v*>(x)[t];
         f32x4v o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int c = c0 + q;
-            const float rstd = save[C + c];
-            const float xh = (xv[q] - save[c]) * rstd;
-            o[q] = gamma[c] * rstd * (gv[q] - red[c] * inv - xh * red[C + c] * inv);
-        }
+        for (int q = 0; q < 4; ++q) o[q] = k1[q] * (gv[q] - r0[q] - (xv[q] - mean[q]) * r1[q]);
         reinterpret_cast<f32x4v*>(dx)[t] = o;
     }
 }
@@ -1022,8 +1044,13 @@ IMK_EXPORT int imk_bn_apply_f32(const float* x, const float* save, const float* 
                                 const float* res, float* y, long R, int C, int relu, void* stream) {
     if (C % 4) return -100;
     const long n4 = R * C / 4;
-    hipLaunchKernelGGL(bn_apply_f32_kernel, dim3(sgrid(n4)), dim3(256), 0, (hipStream_t)stream, x, save, gamma, beta,
-                       res, y, n4, C, relu);
+    const int grid = sgrid(n4);
+    if ((long)grid * 1024 % C == 0)
+        hipLaunchKernelGGL(bn_apply_f32_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, save, gamma,
+                           beta, res, y, n4, C, relu);
+    else
+        hipLaunchKernelGGL(bn_apply_f32_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, save, gamma,
+                           beta, res, y, n4, C, relu);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -1042,8 +1069,13 @@ IMK_EXPORT int imk_bn_bwd_f32(const float* g, const float* y, const float* x, co
                        dgamma, dbeta, C);
     IMK_CHECK_LAUNCH();
     const long n4 = R * C / 4;
-    hipLaunchKernelGGL(bn_bwd_apply_f32_kernel, dim3(sgrid(n4)), dim3(256), 0, (hipStream_t)stream, g, y, x, save,
-                       gamma, red, dx, dres, n4, C, 1.f / (float)R);
+    const int grid = sgrid(n4);
+    if ((long)grid * 1024 % C == 0)
+        hipLaunchKernelGGL(bn_bwd_apply_f32_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, g, y, x, save,
+                           gamma, red, dx, dres, n4, C, 1.f / (float)R);
+    else
+        hipLaunchKernelGGL(bn_bwd_apply_f32_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, g, y, x,
+                           save, gamma, red, dx, dres, n4, C, 1.f / (float)R);
     IMK_CHECK_LAUNCH();
     return 0;
 }
