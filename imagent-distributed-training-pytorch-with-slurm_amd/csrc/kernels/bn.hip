@@ -24,6 +24,8 @@
 // registers, loads/stores are 16 B per lane (cdna_hip_programming.md G13).
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #include "common.h"
 
@@ -623,6 +625,41 @@ bool bn_nt() {
     return v;
 }
 
+// Streaming passes size their grid by grid_for (<= 2048 blocks = 8 per CU); a variant whose registers allow
+// fewer resident blocks per CU (bn_fwd mode 1: 94 VGPRs, 5 waves / SIMD) then runs its grid-stride loop in
+// 1.6 "rounds", the last one on 60 % of the slots. resident_grid caps the grid at what fits at once
+// (IMAGENT_BN_RESIDENT=0: off, for A/B).
+bool bn_resident() {
+    static const bool v = [] {
+        const char* e = getenv("IMAGENT_BN_RESIDENT");
+        return !e || atoi(e) != 0;
+    }();
+    return v;
+}
+
+int resident_grid(const void* kernel, int grid) {
+    if (!bn_resident()) return grid;
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> cap;
+    static int ncu = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = -1;
+    }
+    if (ncu < 0) return grid;
+    auto it = cap.find(kernel);
+    if (it == cap.end()) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
+            per_cu = 1 << 20;  // unknown: no cap
+        it = cap.emplace(kernel, per_cu * ncu).first;
+    }
+    return grid < it->second ? grid : it->second;
+}
+
 int grid_for(long R, int C) {
     const int rpb = 256 / (C / 8);
     long blocks = (R + U * rpb - 1) / (U * rpb);
@@ -648,7 +685,8 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
     hipStream_t st = (hipStream_t)stream;
     const bool nt = bn_nt(), q8 = y8 != nullptr;
 #define LK(M, RL, NT, Q8)                                                                               \
-    hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>), dim3(grid), dim3(256), 0, st, (const bf16_t*)x, sums, \
+    hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>),                                                  \
+                       dim3(resident_grid((const void*)bn_fwd_kernel<M, RL, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)x, sums, \
                        gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, R, C,   \
                        inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym)
 #define L(M, RL)                                              \
@@ -714,7 +752,8 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     const float inv_cnt = 1.f / (float)R;
     const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1];
 #define LK(M, NT, Q8)                                                                                \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8>), dim3(grid), dim3(256), 0, st, (const bf16_t*)g, \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8>),                                               \
+                       dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
                        nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr,       \
                        (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,               \
                        dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8)
