@@ -769,75 +769,6 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     return 0;
 }
 
-// ---- BatchNorm backward folded into the consumer conv's dgrad (ops/conv.py igemm_dgrad_bnfold)
-// The apply pass computes dx = k1 g + k2 + k3 (x - mean) per channel (bn_bwd_apply_kernel);
-// written as dx = A g + B x + Cc the consumer can take (g, x) instead of dx: its dgrad is
-// linear in dx, so dgrad(dx) = dgrad_{W diag(A)}(g) + dgrad_{W diag(B)}(x) + W Cc.
-// coef [3][C] = (A, B, Cc); dgamma / dbeta accumulate as in the apply pass.
-namespace {
-__global__ void bn_bwd_coef_kernel(const float* __restrict__ slab, const float* __restrict__ save,
-                                   const float* __restrict__ gamma, float* __restrict__ dgamma,
-                                   float* __restrict__ dbeta, float* __restrict__ coef, int S, int C,
-                                   float inv_cnt) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float sgx = 0.f, sg = 0.f;  // slot order as stats_finalize_kernel
-    for (int s = 0; s < S; ++s) {
-        sgx += slab[(size_t)s * 3 * C + c];
-        sg += slab[(size_t)s * 3 * C + C + c];
-    }
-    if (dgamma) dgamma[c] += sgx;
-    if (dbeta) dbeta[c] += sg;
-    const float mean = save[c], rstd = save[C + c], gr = gamma[c] * rstd;
-    const float k2 = -gr * inv_cnt * sg, k3 = -gr * inv_cnt * sgx * rstd;
-    coef[c] = gr;
-    coef[C + c] = k3;
-    coef[2 * C + c] = k2 - k3 * mean;
-}
-
-// wt [N][ldw] bf16 (row n = one dgrad output channel, K = C input channels = the BN's channels):
-// wf [N][2C] = [wt diag(A) | wt diag(B)] bf16, bias [N] = wt Cc (fp32)
-__global__ __launch_bounds__(256) void bnfold_weights_kernel(const bf16_t* __restrict__ wt, int ldw,
-                                                             const float* __restrict__ coef,
-                                                             bf16_t* __restrict__ wf, float* __restrict__ bias,
-                                                             int C) {
-    const int n = blockIdx.x;
-    float part = 0.f;
-    for (int k = threadIdx.x; k < C; k += 256) {
-        const float w = bf2f(wt[(size_t)n * ldw + k]);
-        wf[(size_t)n * 2 * C + k] = f2bf(w * coef[k]);
-        wf[(size_t)n * 2 * C + C + k] = f2bf(w * coef[C + k]);
-        part += w * coef[2 * C + k];
-    }
-    __shared__ float red[256];
-    red[threadIdx.x] = part;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) bias[n] = red[0];
-}
-}  // namespace
-
-IMK_EXPORT int imk_bn_bwd_coef(const float* scratch, const float* save, const float* gamma, float* dgamma_acc,
-                               float* dbeta_acc, float* coef, long R, int C, void* stream) {
-    if (R <= 0 || C <= 0) return -100;
-    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, scratch, save,
-                       gamma, dgamma_acc, dbeta_acc, coef, BWD_SLOTS, C, 1.f / (float)R);
-    IMK_CHECK_LAUNCH();
-    return 0;
-}
-
-IMK_EXPORT int imk_bnfold_weights(const void* wt, int ldw, const float* coef, void* wf, float* bias, int N, int C,
-                                  void* stream) {
-    if (N <= 0 || C <= 0 || ldw < C) return -100;
-    hipLaunchKernelGGL(bnfold_weights_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)wt, ldw,
-                       coef, (bf16_t*)wf, bias, C);
-    IMK_CHECK_LAUNCH();
-    return 0;
-}
-
 IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 3) * C; }
 
 // forward statistics: shifted-sum slab [S][2][C] -> out [2][C] = (mean, biased variance)

@@ -56,7 +56,7 @@ __device__ __forceinline__ void unpack8(const u32x4 w, float (&v)[8]) {
 }
 
 template <int W, int R, int EPI>  // EPI 0: forward (+ shifted BN statistics), 1: fused BN backward
-__global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int nbands, int dbg) {
+__global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int nbands) {
     constexpr int PW = halo_pw(W);
     constexpr int PCOLS = W + 2, PROWS = R + 2;
     constexpr int NCH = PROWS * PCOLS * 8;     // 16-B chunks per patch
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         store_patch();
         __syncthreads();
         if (b + 1 < b1) load_patch(b + 1);  // in flight while this band computes
-        if (active && dbg != 2) {
+        if (active) {
             f32x4 acc[4][2];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                         u32x2{pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3])};
                 }
         }
-        if (!active || dbg == 1) continue;
+        if (!active) continue;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -350,11 +350,7 @@ int launch_halo(const IGemmArgs& a, hipStream_t st) {
     const size_t lds = halo_lds(W, R);
     const int nbands = a.N * (a.H / R);
     const int G = std::min(nbands, halo_cus() * halo_blocks_per_cu());
-    static const int dbg = [] {  // profiling only: 1 = no epilogue, 2 = no MFMA loop
-        const char* e = getenv("IMAGENT_HALO_DBG");
-        return e ? atoi(e) : 0;
-    }();
-    hipLaunchKernelGGL((halo3x3_kernel<W, R, EPI>), dim3(G), dim3(512), lds, st, a, nbands, dbg);
+    hipLaunchKernelGGL((halo3x3_kernel<W, R, EPI>), dim3(G), dim3(512), lds, st, a, nbands);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;

@@ -125,7 +125,6 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         return conv_stream(a, st);
     }
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
-    if (a.X2) return conv_stream(a, st);  // folded BN backward: the streaming kernel only
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     if (tile == 0 && a.C == 64 && a.Nout == 64 && a.nth == 3 && a.ntw == 3) {
         const int r = conv_halo(a, st);

@@ -88,10 +88,6 @@ struct IGemmArgs {
     // variance E[(v-s)^2] - E[v-s]^2 has no catastrophic cancellation even when
     // |mean| >> std (imk_bn_stats_finalize turns the slab into mean / variance).
     const float* shift;
-    // conv_stream only: the second half of the K channels comes from X2 (row pitch C / 2 for both):
-    // a BatchNorm backward folded into this dgrad (dgrad(A g + B x + c) = dgrad_{W A}(g) +
-    // dgrad_{W B}(x) + W c, ops/conv.py igemm_dgrad_bnfold), with `bias` = W c added to the sums
-    const bf16_t* X2;
     // conv_stream only: the gathered operand is relu(X * xbn[c] + xbn[C + c]) per input channel c --
     // the producing BatchNorm's apply + ReLU done on the consumer's operand load (ops/block.py),
     // so the BN output is never written

@@ -225,7 +225,7 @@ int launch_v3(const IGemmArgs& a, hipStream_t st) {
 inline bool v3_ok(const IGemmArgs& a) {
     if (a.C % 64 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
     if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_FP8 | IG_AFFINE)) return false;
-    if (a.bias || a.xbn || a.X2 || a.Nout % 8 || a.ldy % 8) return false;
+    if (a.bias || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
     const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
     return xb < (1ull << 31) && wb < (1ull << 31);
 }

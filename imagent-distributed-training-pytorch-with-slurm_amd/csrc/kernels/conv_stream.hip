@@ -161,17 +161,6 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 row = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
             }
         }
-        if (a.X2) {  // K = [X | X2], each with C / 2 channels per row
-            const int ldx = a.C / 2;
-            const bf16_t* p1 = a.X + row * ldx + fq * 8;
-            const bf16_t* p2 = a.X2 + row * ldx + fq * 8;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const bf16_t* q = ks * 32 < ldx ? p1 + ks * 32 : p2 + (ks * 32 - ldx);
-                pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(q) : u32x4{0u, 0u, 0u, 0u};
-            }
-            return;
-        }
         const bf16_t* p = a.X + row * a.C + fq * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
@@ -181,11 +170,6 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     for (int d = 0; d < D; ++d) fetch(d, w0 + d * wstride);
     __syncthreads();  // weight slice visible
 
-    // per-output-channel bias (folded BN backward: W c) of the lane's fixed epilogue channels,
-    // added to the bf16-staged sums (only the X2 path has one)
-    float bias[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) bias[c] = a.bias ? a.bias[n + c] : 0.f;
     int aoff[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((ks * 4 + fq) ^ (fr & SWM)) * 16);
@@ -287,8 +271,8 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     float v[8];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        v[2 * k] = lo_bf(t[k]) + bias[2 * k];
-                        v[2 * k + 1] = hi_bf(t[k]) + bias[2 * k + 1];
+                        v[2 * k] = lo_bf(t[k]);
+                        v[2 * k + 1] = hi_bf(t[k]);
                         if (accum) {
                             v[2 * k] += lo_bf(oo[q][k]);
                             v[2 * k + 1] += hi_bf(oo[q][k]);
@@ -404,17 +388,6 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         return launch_stream1<7 * 32, 64, 2, 0, true>(a, st);
     }
     if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
-    if (a.X2) {  // folded BN backward (K = 2 x 256 -> 64 channels): this kernel or an error
-        if (a.C != 512 || a.Nout != 64 || !(a.flags & IG_BNBWD) || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
-            a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.H != a.OH || a.W != a.OW || a.ldy != a.Nout ||
-            a.ldb < a.C || (a.bnx2 && !a.bnym))
-            return -110;
-        static const int depth = [] {  // IMAGENT_FOLD_D: pixel groups prefetched per wave (A/B)
-            const char* e = getenv("IMAGENT_FOLD_D");
-            return e ? atoi(e) : 1;  // (2 spills: 256 VGPRs + scratch)
-        }();
-        return depth == 1 ? launch_stream<512, 64, 1>(a, st) : launch_stream<512, 64, 2>(a, st);
-    }
     if (a.xbn) {  // BN apply + ReLU on the operand load: K = 64 / 128 plain-epilogue 1x1 convs only
         if ((a.flags & (IG_BNBWD | IG_ACCUM)) || a.bias || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
             a.H != a.OH || a.W != a.OW || a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout ||
@@ -431,17 +404,13 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;
     // K = 256 into > 128 channels (bottleneck conv3 / downsample forwards): 64-channel
     // weight slices resident in LDS, the slices of one pixel range on one XCD (the pixels
-    // are fetched from HBM once and re-read from that XCD's L2). IMAGENT_STREAM_WIDE=0: tiles.
+    // are fetched from HBM once and re-read from that XCD's L2).
     // Only K = 256: at K = 512 the v3 tiles win (conv_bench at 1024 img: 512 -> 2048 @7 fwd 210 -> 179 us,
     // 512 -> 1024 /2 @28 443 -> 375, 2048 -> 512 dgrad 209 -> 152; K = 256 stays here: 256 -> 1024 @14
-    // fwd 264 vs 370). IMAGENT_STREAM_WIDE=2: K = 512 too.
-    static const int wide = [] {
-        const char* e = getenv("IMAGENT_STREAM_WIDE");
-        return e ? atoi(e) : 1;
-    }();
-    if (wide && !(a.flags & IG_BNBWD) && (a.C == 256 || (a.C == 512 && wide == 2)) && a.Nout > 128) {
+    // fwd 264 vs 370).
+    if (!(a.flags & IG_BNBWD) && a.C == 256 && a.Nout > 128) {
         if (bn != 0 && bn != 64) return 1;
-        return a.C == 256 ? launch_stream1<256, 64, 2, 0>(a, st) : launch_stream1<512, 64, 1, 0>(a, st);
+        return launch_stream1<256, 64, 2, 0>(a, st);
     }
     int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (a.flags & IG_BNBWD) {

@@ -36,10 +36,6 @@ struct WgradArgs {
     int m_per_split;   // multiple of BR
     uint32_t mg_ohw, sh_ohw, mg_ow, sh_ow;  // magic division by OH*OW and OW
     int stem;          // bit 0: C == 4 row-segment gather, dW is [Co][KH][32]
-    // folded BatchNorm backward (ops/conv.py conv_wgrad_bnfold): dY is the BN's masked upstream
-    // gradient g and the operand is A g + B x + Cc per channel, x = dYx, coef = [3][Co] (A, B, Cc)
-    const bf16_t* dYx;
-    const float* dYcoef;
     // the X operand is relu(X * xbn[c] + xbn[Ci + c]) (BatchNorm apply + ReLU of the conv's input,
     // never materialised: ops/block.py); out-of-image taps stay 0
     const float* xbn;
@@ -57,7 +53,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t mg, uint32_t sh) {
 // BR: pixels (reduction rows) per stage -- 64, or 32 (half the LDS: three
 // 4-wave blocks per CU instead of two, more waves to hide the load latency)
 // XB: the X operand gets the BatchNorm apply + ReLU of a.xbn while it is staged
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false, bool XB = false>
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XB = false>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgrad_kernel(const WgradArgs a) {
     constexpr int NT = NW * 64;
     constexpr int WKC = NW / WCO;
@@ -108,17 +104,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
         xdw = xkw - a.pad;
     }
 
-    // XF: this thread's 8 dY channels are fixed (dco): their fold coefficients stay in registers
-    float xa[8], xb[8], xc[8];
-    if (XF) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int c = dco_ok ? dco + k : 0;
-            xa[k] = a.dYcoef[c];
-            xb[k] = a.dYcoef[a.Co + c];
-            xc[k] = a.dYcoef[2 * a.Co + c];
-        }
-    }
     // XB: this thread's 8 X channels are fixed (xci): their BN scale / shift stay in registers
     float bsc[8], bsh[8];
     if (XB) {
@@ -130,24 +115,16 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
         }
     }
     bool xok[XB ? X_CH : 1];  // XB: the row exists (padding rows stay 0, not relu(shift))
-    u32x4 rd[D_CH], rx[X_CH], rdx[XF ? D_CH : 1];
-    bool rok[XF ? D_CH : 1];  // XF: the row exists (padding rows must contribute 0, not Cc)
+    u32x4 rd[D_CH], rx[X_CH];
     auto load = [&](int st) {
         const int mb = mbeg + st * BR;
 #pragma unroll
         for (int i = 0; i < D_CH; ++i) {
             const int row = (tid + NT * i) / CPR_D;
             const int m = mb + row;
-            u32x4 v = {0, 0, 0, 0}, w = {0, 0, 0, 0};
-            if (m < mend && dco_ok) {
-                v = *reinterpret_cast<const u32x4*>(a.dY + (size_t)m * a.Co + dco);
-                if (XF) w = *reinterpret_cast<const u32x4*>(a.dYx + (size_t)m * a.Co + dco);
-            }
+            u32x4 v = {0, 0, 0, 0};
+            if (m < mend && dco_ok) v = *reinterpret_cast<const u32x4*>(a.dY + (size_t)m * a.Co + dco);
             rd[i] = v;
-            if (XF) {
-                rdx[i] = w;
-                rok[i] = m < mend && dco_ok;
-            }
         }
 #pragma unroll
         for (int i = 0; i < X_CH; ++i) {
@@ -184,17 +161,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
 #pragma unroll
         for (int i = 0; i < D_CH; ++i) {
             const int id = tid + NT * i;
-            u32x4 v = rd[i];
-            if (XF) {  // dA = A g + B x + Cc, rounded to bf16 as the apply pass would store it
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float lo = xa[2 * k] * lo_bf(rd[i][k]) + xb[2 * k] * lo_bf(rdx[i][k]) + xc[2 * k];
-                    const float hi =
-                        xa[2 * k + 1] * hi_bf(rd[i][k]) + xb[2 * k + 1] * hi_bf(rdx[i][k]) + xc[2 * k + 1];
-                    v[k] = rok[i] ? pack_bf2(lo, hi) : 0u;
-                }
-            }
-            *reinterpret_cast<u32x4*>(d + (id / CPR_D) * PCO + (id % CPR_D) * 16) = v;
+            *reinterpret_cast<u32x4*>(d + (id / CPR_D) * PCO + (id % CPR_D) * 16) = rd[i];
         }
 #pragma unroll
         for (int i = 0; i < X_CH; ++i) {
@@ -288,15 +255,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
 
 namespace {
 
-int xf_target() {  // IMAGENT_WGRAD_XF_TARGET: blocks of a folded-BN wgrad (0: the generic target)
-    static const int t = [] {
-        const char* e = getenv("IMAGENT_WGRAD_XF_TARGET");
-        return e ? atoi(e) : 0;
-    }();
-    return t;
-}
-
-template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XF = false, bool XB = false>
+template <int BCO, int BKC, int WCO, bool STEM, int NW = 4, int BR = 64, bool XB = false>
 int launch1(WgradArgs a, int splits, hipStream_t st) {
     const int K = STEM ? a.KH * 32 : a.KH * a.KW * a.Ci;
     const int ntiles = ((a.Co + BCO - 1) / BCO) * ((K + BKC - 1) / BKC);
@@ -313,9 +272,6 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
         int target = NW == 4 ? 768 : 512;
         if (NW == 4 && STEM) target = 1280;
         else if (NW == 4 && a.KH * a.KW > 1 && a.Ci <= 128) target = 1024;
-        // folded BN backward: IMAGENT_WGRAD_XF_TARGET blocks (shorter blocks let the main stream's
-        // small kernels queued behind this grid in sooner; 768 / 2048 / 4096 measured alike)
-        if (XF && xf_target() > 0) target = xf_target();
         if (tgt_env > 0) target = tgt_env;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
@@ -326,7 +282,7 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)2 * BR * ((BCO * 2 + 32) + (BKC * 2 + 32));
-    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR, XF, XB>), dim3(ntiles * splits), dim3(NW * 64), lds,
+    hipLaunchKernelGGL((wgrad_kernel<BCO, BKC, WCO, STEM, NW, BR, XB>), dim3(ntiles * splits), dim3(NW * 64), lds,
                        st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
@@ -335,21 +291,14 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
 
 // Stage depth by shape (measured, 1x MI355X, R50 @ 512 img): 32-row stages win
 // on 1x1 convs, the stem and 64-channel tiles (-8..-20 %), 64-row stages on
-// the 3x3 convs with 128x128 tiles (-15..-25 % vs 32). IMAGENT_WGRAD_BR=32|64
-// forces one.
+// the 3x3 convs with 128x128 tiles (-15..-25 % vs 32).
 template <int BCO, int BKC, int WCO, bool STEM>
 int launch(WgradArgs a, int splits, hipStream_t st) {
-    static const int force = [] {
-        const char* e = getenv("IMAGENT_WGRAD_BR");
-        return e ? atoi(e) : 0;
-    }();
-    const bool br32 = force ? force == 32 : (STEM || BCO == 64 || a.KH * a.KW == 1);
+    const bool br32 = STEM || BCO == 64 || a.KH * a.KW == 1;
     if constexpr (!STEM) {
-        if (a.dYx)  // folded BN backward: 1x1 convs only (ops/conv.py conv_wgrad_bnfold)
-            return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, true>(a, splits, st) : -110;
         if (a.xbn)  // BN apply + ReLU of X on the staging path (padding taps stay 0)
-            return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, false, true>(a, splits, st)
-                        : launch1<BCO, BKC, WCO, STEM, 4, 64, false, true>(a, splits, st);
+            return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32, true>(a, splits, st)
+                        : launch1<BCO, BKC, WCO, STEM, 4, 64, true>(a, splits, st);
     }
     return br32 ? launch1<BCO, BKC, WCO, STEM, 4, 32>(a, splits, st)
                 : launch1<BCO, BKC, WCO, STEM, 4, 64>(a, splits, st);
@@ -361,8 +310,7 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     const WgradArgs& a = *args;
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if ((a.stem & 1) && (a.dYx || a.xbn)) return -110;
-    if (a.dYx && a.xbn) return -111;
+    if ((a.stem & 1) && a.xbn) return -110;
     if (a.stem & 1) {
         if (a.Ci != 4 || a.KW > 8 || a.Co % 8) return -102;
         return launch<64, 128, 1, true>(a, splits, st);
@@ -408,7 +356,7 @@ IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int var
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (variant < 0) {
-        if (a.stem || a.dYx || a.xbn || a.Ci % 8 || a.Co % 8) return -106;
+        if (a.stem || a.xbn || a.Ci % 8 || a.Co % 8) return -106;
         return a.Co <= 64 ? launch<64, 128, 1, false>(a, splits, st) : launch<128, 128, 2, false>(a, splits, st);
     }
     if (variant == 9) return wgrad_halo_ok(a) ? launch_wgrad_halo(a, st) : -106;

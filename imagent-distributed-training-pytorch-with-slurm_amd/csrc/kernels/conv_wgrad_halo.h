@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
 // the shapes this kernel covers (host); wide = false: only 64 -> 64 (IMAGENT_WGRAD_HALO=1, A/B); dflt: the
 // shapes the default dispatch gives it
 inline bool wgrad_halo_ok(const WgradArgs& a, bool wide = true, bool dflt = false) {
-    if (a.stem || a.dYx || a.xbn) return false;
+    if (a.stem || a.xbn) return false;
     if (a.Ci % 64 || a.Co % 64 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1) return false;
     if (!wide && (a.Ci != 64 || a.Co != 64)) return false;
     if (a.OW != a.W || a.OH != a.H) return false;

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
 // shapes this kernel covers (host): one tap per 128-wide k tile, whole 128-channel co tiles,
 // byte offsets of both operands below 2^31
 bool wgrad_v3_ok(const WgradArgs& a) {
-    if (a.stem || a.dYx || a.xbn || a.Ci % 128 || a.Co % 128) return false;
+    if (a.stem || a.xbn || a.Ci % 128 || a.Co % 128) return false;
     if ((size_t)a.M * a.Co * 2 >= (1u << 31) || (size_t)a.N * a.H * a.W * a.Ci * 2 >= (1u << 31)) return false;
     return true;
 }

@@ -86,7 +86,7 @@ class IGemmArgs(C.Structure):
         ("flags", C.c_int),
         ("bnx", C.c_void_p), ("bnym", C.c_void_p), ("bnsave", C.c_void_p), ("bngamma", C.c_void_p),
         ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
-        ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p), ("X2", C.c_void_p),
+        ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p),
         ("xbn", C.c_void_p),
     ]
 
@@ -111,7 +111,7 @@ class WgradArgs(C.Structure):
         ("KH", C.c_int), ("KW", C.c_int), ("stride", C.c_int), ("pad", C.c_int),
         ("m_per_split", C.c_int),
         ("mg_ohw", C.c_uint32), ("sh_ohw", C.c_uint32), ("mg_ow", C.c_uint32), ("sh_ow", C.c_uint32),
-        ("stem", C.c_int), ("dYx", C.c_void_p), ("dYcoef", C.c_void_p), ("xbn", C.c_void_p),
+        ("stem", C.c_int), ("xbn", C.c_void_p),
     ]
 
 
@@ -169,8 +169,6 @@ def _declare(name: str, lib) -> None:
             "imk_bn_stats_det": [vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_stats_finalize": [vp, vp, vp, i32, i32, i64, vp],
             "imk_bn_finalize_affine": [vp, vp, vp, vp, vp, vp, i32, i32, i64, f32, i32, vp],
-            "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
-            "imk_bnfold_weights": [vp, i32, vp, vp, vp, i32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_fwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,

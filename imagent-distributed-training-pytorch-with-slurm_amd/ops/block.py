@@ -32,9 +32,8 @@ import torch
 
 from . import streams
 from . import conv as _conv
-from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_bwd_coef, bn_scale_shift
-from .conv import (BNBwdFuse, bnfold_ok, conv_wgrad, conv_wgrad_bnfold, igemm_dgrad, igemm_dgrad_bnfold,
-                   igemm_fwd)
+from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_scale_shift
+from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
 # Issue each weight gradient after the BN-backward pass that follows its dgrad, so the side
@@ -62,7 +61,7 @@ _HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
 
 def _xfuse_ok(conv, a, q) -> bool:
     """Can ``conv`` (the consumer of BN(a) + ReLU) apply that BN on its operand path?"""
-    if not (_XFUSE and q is None and a.is_cuda) or _conv._BNFOLD or _conv._NOSTREAM:
+    if not (_XFUSE and q is None and a.is_cuda) or _conv._NOSTREAM:
         return False
     if conv.kh == 1 and conv.kw == 1:
         return (conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
@@ -100,23 +99,11 @@ def _dg8(d8, conv):
     return (d8[0], d8[1], conv.wt8, conv.w8_exp)
 
 
-class _Folded:
-    """A BatchNorm-backward output dx = A g + B x + Cc kept as (g, x, coef): the
-    consumer conv's dgrad and wgrad take it directly (``ops.bn.bn_bwd_coef``)."""
-
-    __slots__ = ("g", "x", "coef")
-
-    def __init__(self, g, x, coef):
-        self.g, self.x, self.coef = g, x, coef
-
-
 def _wgrad(conv, dA, h):
     """``h`` is the conv's input, or (BN input, scale / shift) when the BN + ReLU before it is
     applied on the operand path (``IMAGENT_BN_XFUSE``)."""
     if isinstance(h, tuple):
         conv_wgrad(conv, dA, h[0], xbn=h[1])
-    elif isinstance(dA, _Folded):
-        conv_wgrad_bnfold(conv, dA.g, dA.x, dA.coef, h)
     else:
         conv_wgrad(conv, dA, h)
 
@@ -232,20 +219,15 @@ class BlockFn(torch.autograd.Function):
                              fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
         elif premasked:
-            if q is None and fuse and n >= 2 and bnfold_ok(conv_l, dout, BNBwdFuse(acts[-1], pairs[-2][1])):
-                # the last BN's backward folded into conv_l's dgrad / wgrad: no dA pass
-                dA = _Folded(dout, a_last, bn_bwd_coef(bn_l, a_last.numel() // a_last.shape[-1]))
-            else:
-                g8a = q.grad_out(a_last, bn_l) if q is not None else None
-                dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
-                dA8 = _use8(q, g8a)
+            g8a = q.grad_out(a_last, bn_l) if q is not None else None
+            dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
+            dA8 = _use8(q, g8a)
             dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
         else:
             dA, dX = bn_act_backward(dout, a_last, x, out, bn_l, None, 1, True)  # dX = masked dout
         streams.flush_deferred()  # the next block's conv1 wgrad, after this memory-bound BN pass
         block._last_bn = None
         block._bnb_done = False
-        fold_done = None  # side-stream event after a folded wgrad that reads dout (= dX, accumulated below)
         xbn = ctx.xbn  # xbn[i]: conv i's input is BN(acts[i - 1]) + ReLU applied on its operand path
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
@@ -253,11 +235,8 @@ class BlockFn(torch.autograd.Function):
             if i > 0:
                 bn_prev = pairs[i - 1][1]
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
-                if isinstance(dA, _Folded):
-                    dH = igemm_dgrad_bnfold(dA.g, dA.x, dA.coef, conv, fz)
-                else:
-                    dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
-                                     conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
+                dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
+                                 conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
                 if h_in is None:  # xfuse: the weight gradient applies the BN on its operand staging
                     h_in = (acts[i - 1], xbn[i])
                 if not _DEFER_WGRAD:
@@ -274,11 +253,6 @@ class BlockFn(torch.autograd.Function):
                     # issued after the BN-backward pass: the side-stream weight gradient then runs
                     # beside the next (compute-bound) dgrad instead of the memory-bound BN pass
                     _wgrad(conv, dA_w, h_in)
-                if isinstance(dA_w, _Folded) and dA_w.g.is_cuda:
-                    side = streams.active_side_stream()
-                    if side is not None:  # conv1's dgrad below accumulates into dout: after this read
-                        fold_done = torch.cuda.Event()
-                        fold_done.record(side)
             else:
                 prev = getattr(block, "_prev_block", None)
                 fz = None
@@ -287,8 +261,6 @@ class BlockFn(torch.autograd.Function):
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
                     fz = BNBwdFuse(pa, pbn, y=pym, x2=pad_, bn2=pds[1] if pds is not None else None)
-                if fold_done is not None:
-                    torch.cuda.current_stream().wait_event(fold_done)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
                             accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
                 if _DEFER_WGRAD:  # issued by the previous block's backward after its BN pass

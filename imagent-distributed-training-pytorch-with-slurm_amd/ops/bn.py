@@ -151,24 +151,6 @@ def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tenso
     return dx, dx2
 
 
-def bn_bwd_coef(bn, rows: int) -> torch.Tensor:
-    """BatchNorm backward as per-channel coefficients instead of an apply pass:
-    for a gradient ``g`` that its producing dgrad ReLU-masked and reduced into
-    ``bn.work.scratch`` (``BNBwdFuse``), dx = A g + B x + Cc; returns coef
-    [3, C] = (A, B, Cc) and accumulates dgamma / dbeta as the apply pass does.
-    The consumer conv then takes (g, x) (``ops.conv.igemm_dgrad_bnfold`` /
-    ``conv_wgrad_bnfold``): the full-size dx is never written or read."""
-    w = bn.work
-    C = bn.weight.shape[0]
-    coef = torch.empty((3, C), device=bn.weight.device, dtype=torch.float32)
-    _lib.check(_lib.kernels().imk_bn_bwd_coef(w.scratch.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
-                                              bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(), coef.data_ptr(),
-                                              rows, C, _lib.stream_ptr()), "bn bwd coef")
-    notify_ready(bn.weight)
-    notify_ready(bn.bias)
-    return coef
-
-
 def _g8desc(g8):
     if g8 is None or (g8[0] is None and g8[1] is None):
         return None

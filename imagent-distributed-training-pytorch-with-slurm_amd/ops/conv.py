@@ -96,11 +96,6 @@ _EPI_FLAGS = {0: 0, 1: 128, 2: 64}
 _NOSTREAM = 2048 if os.environ.get("IMAGENT_CONV_STREAM", "1") == "0" else 0
 # IMAGENT_BN_SHIFT=0: forward BN statistics as raw sums (shift 0) -- A/B switch
 _SHIFT = os.environ.get("IMAGENT_BN_SHIFT", "1") != "0"
-# IMAGENT_BN_FOLD=1: fold the stage-1 bottleneck conv3's BatchNorm backward into its dgrad / wgrad
-# (bnfold_ok). Measured neutral at R50 / 1024 (-0.3 .. +0.6 % across boxes): the 2 x 1.8 ms apply
-# passes go, but the K = 512 streaming dgrad (1.4 ms vs 0.45) and the longer side-stream wgrad
-# starve the main stream's small kernels (profiles/r50_round2_schedule_experiments.md). Off by default.
-_BNFOLD = os.environ.get("IMAGENT_BN_FOLD", "0") == "1"
 
 
 def set_stream(enabled: bool) -> None:
@@ -340,71 +335,6 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
                    f"conv wgrad variant {variant}")
         return
     _wgrad_call(a, splits, _lib.stream_ptr(), "conv wgrad")
-
-
-def bnfold_ok(conv, g: torch.Tensor, bnb: Optional["BNBwdFuse"]) -> bool:
-    """Can conv's dgrad / wgrad take a folded BatchNorm backward (g, x, coef) instead of
-    dx? The streaming kernel covers 1x1 stride-1 256 -> 64 dgrads with a fused
-    BN-backward epilogue (conv_stream.hip, X2); the wgrad's register staging any 1x1."""
-    return (_BNFOLD and g.is_cuda and conv.kh == 1 and conv.kw == 1 and conv.stride == 1 and conv.padding == 0
-            and conv.out_channels == 256 and conv.in_channels == 64 and bnb is not None and
-            (bnb.x2 is None or bnb.y is not None) and not _NOSTREAM)
-
-
-def igemm_dgrad_bnfold(g: torch.Tensor, x: torch.Tensor, coef: torch.Tensor, conv,
-                       bnb: "BNBwdFuse") -> torch.Tensor:
-    """dgrad(A g + B x + Cc) of a 1x1 stride-1 conv, without materialising the
-    BatchNorm-backward output: the weights are scaled per input channel into
-    [W diag(A) | W diag(B)] (K doubles: the streaming kernel reads g and x side
-    by side) and W Cc is added as a bias before the fused BN-backward epilogue of
-    the NEXT BatchNorm (``bnb``). See :func:`ops.bn.bn_bwd_coef`."""
-    N, H, W, Co = g.shape
-    wt = conv.wt_bf16  # [Ci][1][1][Co]
-    Ci = wt.shape[0]
-    k = _lib.kernels()
-    st = _lib.stream_ptr()
-    wf = torch.empty((Ci, 2 * Co), device=g.device, dtype=torch.bfloat16)
-    bias = torch.empty((Ci,), device=g.device, dtype=torch.float32)
-    _lib.check(k.imk_bnfold_weights(wt.data_ptr(), Co, coef.data_ptr(), wf.data_ptr(), bias.data_ptr(), Ci, Co, st),
-               "bnfold weights")
-    out = torch.empty((N, H, W, Ci), device=g.device, dtype=torch.bfloat16)
-    a = _base_args(g.data_ptr(), wf.data_ptr(), out.data_ptr(), N, H, W, 2 * Co, H, W, Ci, 2 * Co, 1)
-    a.X2 = x.data_ptr()
-    a.bias = bias.data_ptr()
-    a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = 1, 1, 0, 1, 0, 1
-    a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, 1
-    a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, 1, 0, 0, Ci
-    a.flags = 0
-    bnb.fill(a)
-    _igemm_call(a, 0, st, "conv dgrad (folded BN backward)")
-    return out
-
-
-def conv_wgrad_bnfold(mod, g: torch.Tensor, x: torch.Tensor, coef: torch.Tensor, h: torch.Tensor) -> None:
-    """:func:`conv_wgrad` of dY = A g + B x + Cc (folded BatchNorm backward): the
-    wgrad kernel builds each dY chunk in its register staging."""
-    side = streams.side_stream(g.device) if g.is_cuda else None
-    ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
-    if side is not None:
-        side.wait_stream(torch.cuda.current_stream(g.device))
-    with ctx:
-        N, Hh, Ww, Ci = h.shape
-        _, OH, OW, Co = g.shape
-        a = _lib.WgradArgs()
-        a.stem = 0
-        a.dY, a.X, a.dW = g.data_ptr(), h.data_ptr(), mod.weight.grad.data_ptr()
-        a.dYx, a.dYcoef = x.data_ptr(), coef.data_ptr()
-        a.N, a.H, a.W, a.Ci, a.Co = N, Hh, Ww, Ci, Co
-        a.OH, a.OW, a.M = OH, OW, N * OH * OW
-        a.KH, a.KW, a.stride, a.pad = 1, 1, 1, 0
-        a.m_per_split = 0
-        a.mg_ohw, a.sh_ohw = _magic(OH * OW)
-        a.mg_ow, a.sh_ow = _magic(OW)
-        _wgrad_call(a, 0, _lib.stream_ptr(), "conv wgrad (folded BN)")
-        notify_ready(mod.weight)
-    if side is not None:
-        streams.protect(g, x, coef, h)
-        streams.ensure_join_after_backward()
 
 
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor) -> None:

@@ -684,75 +684,3 @@ def test_halo_conv3x3(shape):
     assert rel(dx.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
-def test_bn_fold_ops():
-    """BatchNorm backward folded into a 1x1 conv's dgrad and wgrad (bn_bwd_coef,
-    igemm_dgrad_bnfold, conv_wgrad_bnfold) vs the apply pass followed by the
-    plain dgrad (with the next BN's fused backward epilogue) and wgrad."""
-    import types
-    from imagent_amd.models.resnet import BatchNorm2d, BNWork
-    from imagent_amd.ops import _lib, streams
-    from imagent_amd.ops.bn import bn_apply_backward, bn_bwd_coef
-    from imagent_amd.ops.conv import BNBwdFuse, conv_wgrad_bnfold, igemm_dgrad, igemm_dgrad_bnfold, igemm_wgrad
-    streams.set_wgrad_overlap(False)
-    torch.manual_seed(11)
-    N, H, C3, C2 = 4, 14, 256, 64
-    R = N * H * H
-    nsc = _lib.kernels().imk_bn_bwd_scratch_floats(C3)
-    slots = (nsc // C3 - 3) // 3
-
-    def make_bn(C, xin):
-        bn = BatchNorm2d(C).to(DEV)
-        with torch.no_grad():
-            bn.weight.uniform_(0.5, 1.5)
-            bn.bias.uniform_(-0.5, 0.5)
-        mean = xin.float().reshape(-1, C).mean(0)
-        rstd = torch.rsqrt(xin.float().reshape(-1, C).var(0, unbiased=False) + 1e-5)
-        bn.work = BNWork(None, None, torch.stack([mean, rstd]).contiguous(),
-                         torch.zeros(_lib.kernels().imk_bn_bwd_scratch_floats(C), device=DEV))
-        bn.weight.grad = torch.zeros_like(bn.weight)
-        bn.bias.grad = torch.zeros_like(bn.bias)
-        return bn, mean, rstd
-
-    a3 = bf(torch.randn(N, H, H, C3, device=DEV) * 2 + 0.3)
-    g = bf(torch.randn(N, H, H, C3, device=DEV) * (torch.rand(N, H, H, C3, device=DEV) > 0.4))
-    bn3, m3, r3 = make_bn(C3, a3)
-    xhat3 = (a3.float() - m3) * r3
-    sl = bn3.work.scratch[: slots * 3 * C3].view(slots, 3, C3)
-    sl[0, 0] = (g.float() * xhat3).reshape(-1, C3).sum(0)
-    sl[0, 1] = g.float().reshape(-1, C3).sum(0)
-    a2 = bf(torch.randn(N, H, H, C2, device=DEV))
-    h2 = bf(torch.relu(torch.randn(N, H, H, C2, device=DEV)))
-    w = bf(torch.randn(C3, C2, device=DEV) * 0.1)  # conv3 [Co = 256][Ci = 64]
-    conv = types.SimpleNamespace(kh=1, kw=1, stride=1, padding=0, in_channels=C2, out_channels=C3,
-                                 wt_bf16=w.t().contiguous().view(C2, 1, 1, C3),
-                                 weight=torch.zeros(C3, C2, 1, 1, device=DEV))
-    conv.weight.grad = torch.zeros(C3, C2, 1, 1, device=DEV)
-
-    # apply path
-    bn2a, _, _ = make_bn(C2, a2)
-    dA, _ = bn_apply_backward(g, a3, None, bn3, None, 1)
-    dga, dba = bn3.weight.grad.clone(), bn3.bias.grad.clone()
-    dh_a = igemm_dgrad(dA, conv.wt_bf16, (H, H), 1, 0, 1, 1, bnb=BNBwdFuse(a2, bn2a))
-    dw_a = torch.zeros(C3, C2, device=DEV)
-    igemm_wgrad(dA, h2, dw_a, 1, 0, 1, 1)
-    # folded path
-    bn3.weight.grad.zero_()
-    bn3.bias.grad.zero_()
-    bn2b, _, _ = make_bn(C2, a2)
-    with torch.no_grad():  # the same BN (its mask comes from gamma / beta)
-        bn2b.weight.copy_(bn2a.weight)
-        bn2b.bias.copy_(bn2a.bias)
-    coef = bn_bwd_coef(bn3, R)
-    dh_b = igemm_dgrad_bnfold(g, a3, coef, conv, BNBwdFuse(a2, bn2b))
-    conv_wgrad_bnfold(conv, g, a3, coef, h2)
-    torch.cuda.synchronize()
-    assert torch.allclose(bn3.weight.grad, dga, rtol=1e-6, atol=0) and torch.allclose(bn3.bias.grad, dba, rtol=1e-6)
-    dx_ref = coef[0] * g.float() + coef[1] * a3.float() + coef[2]
-    assert rel(dA, dx_ref) < 1e-2  # the coefficients describe the apply pass
-    assert rel(dh_b, dh_a) < 2e-2, rel(dh_b, dh_a)
-    n2 = _lib.kernels().imk_bn_bwd_scratch_floats(C2)
-    k2 = (n2 // C2 - 3) // 3
-    sa = bn2a.work.scratch[: k2 * 3 * C2].view(k2, 3, C2).sum(0)
-    sb = bn2b.work.scratch[: k2 * 3 * C2].view(k2, 3, C2).sum(0)
-    assert rel(sb[0], sa[0]) < 2e-2 and rel(sb[1], sa[1]) < 2e-2, (rel(sb[0], sa[0]), rel(sb[1], sa[1]))
-    assert rel(conv.weight.grad.view(C3, C2), dw_a) < 1e-2, rel(conv.weight.grad.view(C3, C2), dw_a)

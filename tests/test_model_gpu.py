@@ -162,58 +162,6 @@ def test_fused_bn_backward_matches_unfused(arch):
     assert e_f < max(0.05, 1.3 * e_u + 0.03), (e_u, e_f)
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_bn_fold_matches_apply(overlap, monkeypatch):
-    """BatchNorm backward folded into the consumer conv (ops.bn.bn_bwd_coef: the
-    stage-1 bottleneck conv3 dgrad reads (g, x) with [W diag(A) | W diag(B)] and a
-    W Cc bias, its wgrad builds A g + B x + Cc in registers) vs the apply pass,
-    with and without the weight-gradient side stream (the folded wgrad reads the
-    block's output gradient that conv1's dgrad then accumulates into). Both held
-    to the fp32 oracle as in test_fused_bn_backward_matches_unfused."""
-    from imagent_amd.models import resnet
-    from imagent_amd.models.native import bind_native
-    from imagent_amd.ops import conv as conv_ops
-    torch.manual_seed(3)
-    base = resnet.build("resnet50", num_classes=1000)
-    g = torch.Generator(device=DEV).manual_seed(5)
-    x = torch.randn(8, 48, 48, 4, device=DEV, generator=g).to(torch.bfloat16)
-    x[..., 3] = 0
-    lab = torch.randint(0, 1000, (8,), device=DEV, generator=g)
-    grads = []
-    calls = []
-    real = conv_ops.igemm_dgrad_bnfold
-    monkeypatch.setattr("imagent_amd.ops.block.igemm_dgrad_bnfold",
-                        lambda *a, **k: calls.append(1) or real(*a, **k))
-    for fold in (False, True):
-        monkeypatch.setattr(conv_ops, "_BNFOLD", fold)
-        model = copy.deepcopy(base)
-        st = bind_native(model, DEV, wgrad_overlap=overlap)
-        model.train()
-        st.arena.zero_grad()
-        F.cross_entropy(model(x), lab).backward()
-        torch.cuda.synchronize()
-        grads.append({n: p.grad.float().clone() for n, p in model.named_parameters()})
-    assert len(calls) == 2, calls  # the two stage-1 identity blocks took the folded path
-    ref = copy.deepcopy(base).to(DEV)
-    with torch.no_grad():
-        for p in ref.parameters():
-            p.copy_(p.to(torch.bfloat16).float())
-    ref.train()
-    F.cross_entropy(ref(x[..., :3].float().permute(0, 3, 1, 2).contiguous()), lab).backward()
-    bad = []
-    for n, p in ref.named_parameters():
-        e_u, e_f = rel(grads[0][n], p.grad), rel(grads[1][n], p.grad)
-        if e_u < 0.5 and e_f > max(0.05, 1.3 * e_u + 0.03):
-            bad.append((n, e_u, e_f))
-    assert not bad, bad
-    names = [n for n, _ in ref.named_parameters()]
-    cat = lambda d: torch.cat([d[n].reshape(-1) for n in names])  # noqa: E731
-    want = torch.cat([p.grad.reshape(-1) for _, p in ref.named_parameters()])
-    e_u, e_f = rel(cat(grads[0]), want), rel(cat(grads[1]), want)
-    assert e_f < max(0.05, 1.3 * e_u + 0.03), (e_u, e_f)
-    # (op-level exactness of the folded dgrad / wgrad: test_kernels_gpu.py::test_bn_fold_ops)
-
-
 def _fq(t, e):
     """fake-quantise to OCP e4m3 with scale 2^e (the kernels' saturating rounding)."""
     return (t * 2.0 ** -e).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** e
