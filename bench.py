@@ -85,6 +85,13 @@ def main(argv=None):
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--first-bucket-mb", type=float, default=2.0)
+    ap.add_argument("--grad-allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: all-reduce bf16 copies of the gradient buckets (half the xGMI bytes; fp32 "
+                         "masters and SGD unchanged)")
+    ap.add_argument("--rccl-min-channels", type=int, default=None,
+                    help="NCCL_MIN_NCHANNELS for the RCCL communicator (default: RCCL's choice)")
+    ap.add_argument("--rccl-max-channels", type=int, default=None,
+                    help="NCCL_MAX_NCHANNELS: caps the CUs RCCL's collectives take from the overlapped backward")
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
     ap.add_argument("--wgrad-overlap", type=int, default=1, help="0: weight gradients on the main stream")
     ap.add_argument("--graph", type=int, default=0,
@@ -185,9 +192,14 @@ def main(argv=None):
         else:
             model.to(dev)
             arena = ParamArena(list(model.named_parameters()), dev, order=order)
+        # RCCL reads its channel limits when the communicator is created
+        if a.rccl_min_channels is not None:
+            os.environ["NCCL_MIN_NCHANNELS"] = str(a.rccl_min_channels)
+        if a.rccl_max_channels is not None:
+            os.environ["NCCL_MAX_NCHANNELS"] = str(a.rccl_max_channels)
         comm = make_communicator(ctx, "rccl" if a.kernels == "hip" else "torch" if ctx.world_size > 1 else "local")
         ddp = DataParallel(model, arena, comm, bucket_cap_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
-                           rebuild_buckets=False)
+                           rebuild_buckets=False, grad_reduce_dtype=a.grad_allreduce_dtype)
         if native is not None:  # compute shadows of the rank-0-broadcast masters
             native.refresh_shadows(full=True)
         after = native.refresh_shadows if native else None
@@ -284,9 +296,14 @@ def main(argv=None):
                     "hip_graph": bool(a.graph),
                     "optimizer": "sgd(momentum=0.9, wd=1e-4)" if a.optimizer == "sgd" else
                                  "lars(momentum=0.9, wd=5e-5, eta=1e-3)",
-                    "grad_allreduce": (f"fp32 bucketed {comm.name} avg on the comm stream, "
+                    "grad_allreduce": (f"{a.grad_allreduce_dtype} bucketed {comm.name} avg on the comm stream, "
                                        f"{coll_per_step:g} collectives/step" if coll_per_step > 0 else
                                        "none (world of one, collectives skipped)"),
+                    "grad_allreduce_dtype": a.grad_allreduce_dtype,
+                    "bucket_plan_mb": [round(v, 2) for v in ddp.bucket_sizes_mb()],
+                    "rccl_env": {k: os.environ[k] for k in ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS",
+                                                            "NCCL_P2P_DISABLE", "NCCL_ALGO", "NCCL_PROTO")
+                                 if k in os.environ},
                     "comm": comm.name,
                     "rccl_communicators_per_process": n_rccl,
                     "c10d_backend": ctx.c10d_backend,

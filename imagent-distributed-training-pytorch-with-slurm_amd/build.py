@@ -52,7 +52,8 @@ def _hipcc() -> str:
 def _digest(srcs: List[str], cmd: List[str]) -> str:
     import hashlib
     h = hashlib.sha256()
-    h.update("\0".join(cmd).encode())
+    # paths enter by file name only: the tree is built here and run from another directory on the GPU box
+    h.update("\0".join(os.path.basename(c) if os.path.isabs(c) else c for c in cmd).encode())
     for s in sorted(srcs):
         h.update(os.path.basename(s).encode() + b"\0")
         with open(s, "rb") as f:
@@ -110,16 +111,17 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
 def build_comm(force: bool = False) -> str:
     src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
     out = os.path.join(OUT, "libimagent_comm.so")
-    key = ["comm", ARCH]
-    if not force and not _stale([src], out, key):
-        return out
-    os.makedirs(OUT, exist_ok=True)
     tl = _torch_lib_dir()
     rccl = os.path.join(tl, "librccl.so")
     if not os.path.exists(rccl):
         rccl = os.path.join(_rocm(), "lib", "librccl.so")
-    _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-x", "hip", f"--offload-arch={ARCH}",
-          f"-I{_rocm()}/include", src, "-x", "none", "-o", out, rccl, f"-Wl,-rpath,{tl}"])
+    cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-x", "hip", f"--offload-arch={ARCH}",
+           f"-I{_rocm()}/include", src, "-x", "none", "-o", out, rccl, f"-Wl,-rpath,{tl}"]
+    key = ["comm"] + cmd  # the whole command line: a flag change rebuilds
+    if not force and not _stale([src], out, key):
+        return out
+    os.makedirs(OUT, exist_ok=True)
+    _run(cmd)
     _stamp([src], out, key)
     return out
 
@@ -127,12 +129,13 @@ def build_comm(force: bool = False) -> str:
 def build_runtime(force: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     out = os.path.join(OUT, "libimagent_runtime.so")
-    key = ["runtime"]
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", out] + srcs
+    key = ["runtime"] + cmd  # the whole command line: a flag change rebuilds
     if not force and not _stale(srcs, out, key):
         return out
     os.makedirs(OUT, exist_ok=True)
-    cxx = shutil.which("g++") or "c++"
-    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", out] + srcs)
+    _run(cmd)
     _stamp(srcs, out, key)
     return out
 

@@ -37,8 +37,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="BatchNorm statistics without float atomics (fixed-order reduction passes): two runs "
                         "from the same state give bit-identical statistics (HIP kernels)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"],
-                   help="compute dtype. HIP kernels: bf16 (fp32 masters/accumulation), or fp8 = e4m3 "
-                        "forward convs on the block-scaled MFMA with bf16 backward; fp32 = torch oracle path")
+                   help="compute dtype. HIP kernels: bf16 (fp32 masters/accumulation), fp8 = e4m3 forward "
+                        "convs on the block-scaled MFMA with bf16 backward, fp32 = the reference's precision "
+                        "(imagenet.py:312) on the own exact-f32 MFMA kernels (models/native_f32.py; every ResNet "
+                        "depth, BatchNorm widths up to 2048 channels). --kernels torch: PyTorch ops (oracle)")
     p.add_argument("--data", default="imagenet", choices=["imagenet", "records", "synthetic"],
                    help="imagenet: JPEG folders decoded by worker processes; records: train.imrec / val.imrec "
                         "(python -m imagent_amd.data.records) gathered by the native thread pool")
@@ -73,6 +75,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", default=None)
     p.add_argument("--bucket-mb", type=float, default=16.0)
     p.add_argument("--first-bucket-mb", type=float, default=2.0)
+    p.add_argument("--grad-allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="bf16: all-reduce bf16 copies of the gradient buckets (half the xGMI bytes)")
     p.add_argument("--broadcast-buffers", default="eval", choices=["eval", "always", "never"])
     p.add_argument("--no-rebuild-buckets", dest="rebuild_buckets", action="store_false")
     p.add_argument("--pg-timeout", type=float, default=1800.0)

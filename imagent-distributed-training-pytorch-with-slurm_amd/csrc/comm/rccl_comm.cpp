@@ -54,11 +54,16 @@ thread_local char g_err[512] = {0};
     } while (0)
 
 struct Comm {
+    // written once by init; imc_abort never clears it (readers test `aborting`), so no thread sees a
+    // half-updated handle
     ncclComm_t comm = nullptr;
     // set by imc_abort (the watchdog thread) BEFORE the communicator is torn down: enqueue
     // paths spinning in settle() on the main thread see it and bail out instead of touching
     // a communicator that ncclCommAbort is freeing
     std::atomic<bool> aborting{false};
+    // calls currently inside RCCL with this communicator (InFlight guards); imc_abort waits for it to
+    // drain (bounded) before ncclCommAbort frees the communicator
+    std::atomic<int> inflight{0};
     hipStream_t stream = nullptr;
     int rank = 0, nranks = 1, device = 0, n_events = 64, stream_mode = 0;
     std::vector<hipEvent_t> events;   // ring of reusable events
@@ -135,9 +140,25 @@ static ncclResult_t settle(Comm* c, ncclResult_t r) {
     return r;
 }
 
+// A call's use of the communicator: counted in `inflight` from before the aborting check to the
+// end of the call (sequentially consistent with imc_abort's flag-then-drain, so either the call sees
+// the flag or the abort sees the call).
+struct InFlight {
+    Comm* c;
+    bool ok;
+    explicit InFlight(Comm* c_) : c(c_) {
+        c->inflight.fetch_add(1, std::memory_order_seq_cst);
+        ok = !c->aborting.load(std::memory_order_seq_cst);
+    }
+    ~InFlight() { c->inflight.fetch_sub(1, std::memory_order_seq_cst); }
+    InFlight(const InFlight&) = delete;
+    InFlight& operator=(const InFlight&) = delete;
+};
+
 #define NCCLCALL(c, x)                                                                \
     do {                                                                              \
-        if ((c)->aborting.load(std::memory_order_acquire)) {                          \
+        InFlight g_(c);                                                               \
+        if (!g_.ok) {                                                                 \
             snprintf(g_err, sizeof(g_err), "communicator aborted");                   \
             return -3;                                                                \
         }                                                                             \
@@ -243,8 +264,15 @@ int32_t imc_comm_poll(void* h) {
         return -3;
     }
     ncclResult_t st = ncclSuccess;
-    ncclResult_t q = ncclCommGetAsyncError(c->comm, &st);
-    if (q != ncclSuccess) st = q;
+    {
+        InFlight g(c);
+        if (!g.ok) {
+            snprintf(g_err, sizeof(g_err), "communicator aborted");
+            return -3;
+        }
+        ncclResult_t q = ncclCommGetAsyncError(c->comm, &st);
+        if (q != ncclSuccess) st = q;
+    }
     if (st == ncclInProgress) return 1;
     if (st != ncclSuccess) {
         snprintf(g_err, sizeof(g_err), "ncclCommInitRank: %s", ncclGetErrorString(st));
@@ -263,7 +291,9 @@ int32_t imc_comm_init(const char* id_bytes, int32_t nranks, int32_t rank, int32_
 int32_t imc_comm_nranks(void* h) {
     Comm* c = static_cast<Comm*>(h);
     int n = -1;
-    if (c && c->comm && ncclCommCount(c->comm, &n) != ncclSuccess) n = -1;
+    if (!c || !c->comm) return n;
+    InFlight g(c);
+    if (g.ok && ncclCommCount(c->comm, &n) != ncclSuccess) n = -1;
     return n;
 }
 
@@ -271,7 +301,7 @@ int32_t imc_comm_destroy(void* h) {
     Comm* c = static_cast<Comm*>(h);
     if (!c) return 0;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm) {
+    if (c->comm && !c->aborting.load(std::memory_order_seq_cst)) {
         // a non-blocking communicator finalises asynchronously
         if (settle(c, ncclCommFinalize(c->comm)) == ncclSuccess) ncclCommDestroy(c->comm);
         else ncclCommAbort(c->comm);
@@ -321,6 +351,11 @@ int32_t imc_allreduce_group(void* h, int32_t n, void** ptrs, const uint64_t* cou
     if (src) {
         int32_t rc = imc_stream_join_from(h, src);
         if (rc) return rc;
+    }
+    InFlight g(c);
+    if (!g.ok) {
+        snprintf(g_err, sizeof(g_err), "communicator aborted");
+        return -3;
     }
     NCCLCHK(ncclGroupStart());
     for (int32_t i = 0; i < n; ++i)
@@ -373,22 +408,28 @@ int32_t imc_synchronize(void* h) {
 // state of the communicator (0 == ok).
 int32_t imc_async_error(void* h) {
     Comm* c = static_cast<Comm*>(h);
-    if (!c || !c->comm) return -3;  // aborted
+    if (!c || !c->comm) return -3;
+    InFlight g(c);
+    if (!g.ok) return -3;  // aborted
     ncclResult_t st = ncclSuccess;
     ncclCommGetAsyncError(c->comm, &st);
     return st == ncclInProgress ? 0 : (int32_t)st;
 }
 
-// Failure path (the watchdog thread): flag first, give an enqueue spinning in settle() on
-// another thread a moment to observe the flag and leave, then abort (unblocks kernels waiting
-// on dead peers). The Comm object itself is never freed here.
+// Failure path (the watchdog thread): flag first, wait (bounded) until no call is inside RCCL with
+// this communicator -- an enqueue spinning in settle() sees the flag and leaves -- then abort
+// (unblocks kernels waiting on dead peers). The Comm object and its handle are never freed or
+// cleared here; later calls fail on the flag.
+constexpr double ABORT_DRAIN_S = 5.0;
+
 int32_t imc_abort(void* h) {
     Comm* c = static_cast<Comm*>(h);
-    if (c && !c->aborting.exchange(true, std::memory_order_acq_rel) && c->comm) {
-        std::this_thread::sleep_for(std::chrono::milliseconds(20));
-        ncclComm_t comm = c->comm;
-        c->comm = nullptr;
-        ncclCommAbort(comm);
+    if (c && !c->aborting.exchange(true, std::memory_order_seq_cst) && c->comm) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (c->inflight.load(std::memory_order_seq_cst) > 0 &&
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < ABORT_DRAIN_S)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        ncclCommAbort(c->comm);
     }
     return 0;
 }

@@ -3,6 +3,7 @@
 
 #include "conv_igemm_impl.h"
 #include "conv_igemm_v3.h"
+#include "conv_igemm_v4.h"
 
 // Tile selection (auto, tile 0):
 //  * 64 -> 64 3x3 stride 1: the halo-tiled kernel (conv_halo.hip);
@@ -134,8 +135,17 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // short-K 1x1 convs (K = C = 64 / 128) are HBM streams: weights resident in
     // LDS, pixel fragments straight from HBM (conv_stream.hip); tiles 20/21/22
     // force its 256/128/64-channel slices (A/B testing)
-    const int bn_hint = tile >= 20 ? 256 >> (tile - 20) : 0;
-    if (tile >= 20) tile = 0;
+    if (tile >= 30 && tile <= 33) {  // v4 main loop (conv_igemm_v4.h): one 4-wave block per CU
+        if (!v4_ok(a) || (a.flags & (IG_OUT_F32 | IG_RELU | IG_EPI_DIRECT))) return -105;
+        switch (tile) {
+            case 30: return launch_v4<256, 256, 2, 4, 64, 32>(a, st);
+            case 31: return launch_v4<256, 256, 2, 3, 64, 32>(a, st);
+            case 32: return launch_v4<256, 128, 2, 4, 64, 32>(a, st);
+            default: return launch_v4<128, 256, 2, 4, 64, 32>(a, st);
+        }
+    }
+    const int bn_hint = tile >= 20 && tile <= 22 ? 256 >> (tile - 20) : 0;
+    if (tile >= 20 && tile <= 22) tile = 0;
     const bool autotile = tile == 0;
     if (autotile && a.nth == 1 && a.ntw == 1 && (a.C == 64 || a.C == 128 || a.C == 256 || a.C == 512)) {
         const int r = conv_stream(a, st, bn_hint);

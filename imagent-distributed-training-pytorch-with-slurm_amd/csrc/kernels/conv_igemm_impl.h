@@ -413,9 +413,11 @@ __device__ __forceinline__ void epilogue(const IGemmArgs& a, const f32x4 (&acc)[
 // per channel and quantity into the block's slab slot.
 // (IG_ACCUM adds the old value to the bf16-rounded new one: one extra
 // rounding of the new term versus the direct epilogue.)
-template <int BM, int BN, int NT, int FN, int FM>
-__device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], char* smem, int m0,
-                                             int n0, int wrow0, int wcol0, int lane, int tid, float* st) {
+// The fragment pass (1) is the caller's functor put(smem, P) (it writes this thread's accumulators as
+// bf16 at [pixel row][channel] with row pitch P bytes), so any MFMA shape can feed it.
+template <int BM, int BN, int NT, class Put>
+__device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, char* smem, int m0, int n0, int tid,
+                                                 float* st) {
     constexpr int P = BN * 2 + 16;  // LDS row pitch, bytes
     constexpr int CPR = BN / 8;     // 16-B chunks per row
     constexpr int RG = NT / CPR;    // rows processed concurrently (row groups)
@@ -439,15 +441,8 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
             mean[4 + c] = hi[c];
         }
     }
-    // (1) fragments -> LDS (8 B per lane: 4 channels of one pixel)
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-        for (int i = 0; i < FN; ++i) {
-            const int row = wrow0 + j * 16 + (lane & 15), col = wcol0 + i * 16 + (lane >> 4) * 4;
-            const f32x4 v = acc[i][j];
-            *reinterpret_cast<u32x2*>(smem + row * P + col * 2) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
-        }
+    // (1) fragments -> LDS
+    put(smem, P);
     __syncthreads();
     // (2) row chunks: thread -> fixed channel chunk cc, rows rg + RG*q
     if (bnb && nok) {
@@ -593,6 +588,23 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
         for (int g = 0; g < RG; ++g) sum += red[(qi * RG + g) * BN + ch];
         atomicAdd(st + qi * a.Nout + n0 + ch, sum);
     }
+}
+
+// 16x16x32 fragments (lane: 4 channels of one pixel, 8 B) -> the staged epilogue
+template <int BM, int BN, int NT, int FN, int FM>
+__device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], char* smem, int m0,
+                                             int n0, int wrow0, int wcol0, int lane, int tid, float* st) {
+    auto put = [&](char* sm, int P) {
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int row = wrow0 + j * 16 + (lane & 15), col = wcol0 + i * 16 + (lane >> 4) * 4;
+                const f32x4 v = acc[i][j];
+                *reinterpret_cast<u32x2*>(sm + row * P + col * 2) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+            }
+    };
+    epilogue_lds_put<BM, BN, NT>(a, put, smem, m0, n0, tid, st);
 }
 
 // LDS row swizzle of the stage ring: the 16-B chunk a lane's fragment read or DMA

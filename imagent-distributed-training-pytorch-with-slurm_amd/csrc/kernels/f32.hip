@@ -632,8 +632,11 @@ __global__ __launch_bounds__(256) void bn_partial_f32_kernel(const float* __rest
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ stat,  // shift | mean,rstd
                                                              float* __restrict__ slab, long R, int C) {
-    const int cpr = C / 4, rpb = 256 / cpr, tid = threadIdx.x;
-    const int ch = tid % cpr, c0 = ch * 4;
+    // channel slice blockIdx.y of CW = min(C, 1024) channels (4 per thread): C = 2048 (the ResNet-50/101/152
+    // bottleneck outputs) takes two slices
+    const int CW = C < 1024 ? C : 1024;
+    const int cpr = CW / 4, rpb = 256 / cpr, tid = threadIdx.x;
+    const int ch = tid % cpr, c0 = (int)blockIdx.y * CW + ch * 4;
     const bool active = tid < rpb * cpr;
     f32x4v s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1, sh = s1, rs = s1;
     if (active) {
@@ -669,15 +672,16 @@ __global__ __launch_bounds__(256) void bn_partial_f32_kernel(const float* __rest
         red[1][tid * 4 + q] = s2[q];
     }
     __syncthreads();
-    for (int c = tid; c < C; c += 256) {  // fixed-order fold over the rows of this block
+    for (int c = tid; c < CW; c += 256) {  // fixed-order fold over the rows of this block
         const int cc = c / 4, q = c % 4;
         float a1 = 0.f, a2 = 0.f;
         for (int rr = 0; rr < rpb; ++rr) {
             a1 += red[0][(rr * cpr + cc) * 4 + q];
             a2 += red[1][(rr * cpr + cc) * 4 + q];
         }
-        slab[((size_t)blockIdx.x * 2 + 0) * C + c] = a1;
-        slab[((size_t)blockIdx.x * 2 + 1) * C + c] = a2;
+        const int cg = (int)blockIdx.y * CW + c;
+        slab[((size_t)blockIdx.x * 2 + 0) * C + cg] = a1;
+        slab[((size_t)blockIdx.x * 2 + 1) * C + cg] = a2;
     }
 }
 
@@ -1020,17 +1024,25 @@ IMK_EXPORT int imk_wgrad_f32(const float* dy, const float* x, float* dw, int N, 
 
 IMK_EXPORT int imk_bn_slab_floats_f32(int C) { return BN_MAXB * 2 * C; }
 
+// statistics-pass channel slices (bn_partial_f32_kernel): C <= 1024 with C / 4 dividing 256, or a
+// multiple of 1024 (several 1024-channel slices)
+static bool bn_f32_shape_ok(int C) {
+    if (C % 4 || C <= 0) return false;
+    return C <= 1024 ? 256 % (C / 4) == 0 : C % 1024 == 0;
+}
+static int bn_f32_slices(int C) { return C <= 1024 ? 1 : C / 1024; }
+
 // training forward statistics: save <- (mean, rstd); running stats updated when rmean != null.
 // shift: per-channel values near the mean (the previous batch mean) for the shifted sums.
 IMK_EXPORT int imk_bn_stats_f32(const float* x, const float* shift, float* slab, float* save, float* rmean,
                                 float* rvar, long R, int C, float eps, float momentum, void* stream) {
-    if (C % 4 || 256 % (C / 4) || C > 1024) return -100;
+    if (!bn_f32_shape_ok(C)) return -100;
     const int nb = bn_blocks(R, C);
     // two passes: the mean (sums shifted by the caller's estimate), then the variance as the sum of
     // squares about that mean -- no E[x^2] - E[x]^2 cancellation (PyTorch uses Welford)
     for (int pass = 0; pass < 2; ++pass) {
         const float* sh = pass == 0 ? shift : save;
-        hipLaunchKernelGGL((bn_partial_f32_kernel<false>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nullptr,
+        hipLaunchKernelGGL((bn_partial_f32_kernel<false>), dim3(nb, bn_f32_slices(C)), dim3(256), 0, (hipStream_t)stream, x, nullptr,
                            nullptr, sh, slab, R, C);
         IMK_CHECK_LAUNCH();
         hipLaunchKernelGGL(bn_fold_fwd_f32_kernel, dim3((C + FOLD_CH - 1) / FOLD_CH), dim3(256), 0, (hipStream_t)stream, slab, nb,
@@ -1060,9 +1072,9 @@ IMK_EXPORT int imk_bn_apply_f32(const float* x, const float* save, const float* 
 IMK_EXPORT int imk_bn_bwd_f32(const float* g, const float* y, const float* x, const float* save, const float* gamma,
                               float* slab, float* red, float* dgamma, float* dbeta, float* dx, float* dres, long R,
                               int C, void* stream) {
-    if (C % 4 || 256 % (C / 4) || C > 1024) return -100;
+    if (!bn_f32_shape_ok(C)) return -100;
     const int nb = bn_blocks(R, C);
-    hipLaunchKernelGGL((bn_partial_f32_kernel<true>), dim3(nb), dim3(256), 0, (hipStream_t)stream, x, g, y, save,
+    hipLaunchKernelGGL((bn_partial_f32_kernel<true>), dim3(nb, bn_f32_slices(C)), dim3(256), 0, (hipStream_t)stream, x, g, y, save,
                        slab, R, C);
     IMK_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_fold_bwd_f32_kernel, dim3((C + FOLD_CH - 1) / FOLD_CH), dim3(256), 0, (hipStream_t)stream, slab, nb, red,

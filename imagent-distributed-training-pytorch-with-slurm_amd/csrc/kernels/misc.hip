@@ -552,6 +552,11 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) o[i] = f2bf(p[i]);
 }
 
+__global__ __launch_bounds__(256) void uncast_bf16_kernel(const bf16_t* __restrict__ i_,
+                                                          float* __restrict__ o, long n) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) o[i] = bf2f(i_[i]);
+}
+
 // --------------------------------------------------------- normalize (uint8)
 // in: uint8 [B][Hs][Ws][3] (decoded HWC images), out: bf16 [B][H][W][Cp]
 // out = (x/255 - mean)/std per channel, padded channels 0; per-sample crop
@@ -761,6 +766,14 @@ IMK_EXPORT int imk_sgd(float* p, const float* g, float* buf, void* shadow, long 
 IMK_EXPORT int imk_cast_bf16(const float* p, void* o, long n, void* stream) {
     hipLaunchKernelGGL(cast_bf16_kernel, dim3(stream_grid(n)), dim3(256), 0, (hipStream_t)stream, p,
                        (bf16_t*)o, n);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// bf16 -> fp32 (the bf16 gradient all-reduce writes the reduced buckets back into the fp32 arena)
+IMK_EXPORT int imk_uncast_bf16(const void* i, float* o, long n, void* stream) {
+    hipLaunchKernelGGL(uncast_bf16_kernel, dim3(stream_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)i, o, n);
     IMK_CHECK_LAUNCH();
     return 0;
 }

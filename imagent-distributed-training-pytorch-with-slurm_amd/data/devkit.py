@@ -135,6 +135,15 @@ def _sort_val(d: str, meta_path: str) -> None:
     os.remove(plan_path)
 
 
+def _ready(root: str, split: str) -> bool:
+    """Is ``root/<split>`` already in class-folder layout, with nothing left to do for it?"""
+    d = os.path.join(root, split)
+    if not _has_class_dirs(d) or os.path.exists(os.path.join(d, ".sort_plan.json")):
+        return False
+    # the meta file is only produced when a devkit is there to produce it from
+    return os.path.exists(os.path.join(root, META_FILE)) or not os.path.exists(os.path.join(root, DEVKIT))
+
+
 def prepare(root: str, split: str) -> None:
     """Bring ``root/<split>`` into the ``<wnid>/`` folder layout from the
     archives / devkit that sit in ``root`` (no-op when it already is).
@@ -142,6 +151,8 @@ def prepare(root: str, split: str) -> None:
     Safe to call from every rank at once (a file lock serialises the work) and
     after an interrupted run (scratch-dir extraction, resumable val sort)."""
     if not os.path.isdir(root):
+        return
+    if _ready(root, split):  # nothing to do: no lock (a prepared tree on a read-only mount stays usable)
         return
     with _lock(root):
         import torch

@@ -121,6 +121,7 @@ class NativeState:
 
     def rebind(self) -> None:
         """After an arena re-layout (bucket rebuild): re-point every shadow."""
+        self._aff_dev = None  # the eval-affine table holds raw pointers into the old arena: rebuild it lazily
         self._bind_shadows()
         if self.fp8 is not None:
             self.fp8 = Fp8State(self)

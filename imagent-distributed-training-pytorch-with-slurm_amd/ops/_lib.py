@@ -182,6 +182,7 @@ def _declare(name: str, lib) -> None:
             "imk_colsum_bf16": [vp, vp, i32, i32, vp],
             "imk_sgd": [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, f32, vp],
             "imk_cast_bf16": [vp, vp, i64, vp],
+            "imk_uncast_bf16": [vp, vp, i64, vp],
             "imk_normalize_u8": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_transpose_batched": [vp, i32, i32, vp],
             "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [], "imk_bn_affdesc_size": [],

@@ -159,6 +159,12 @@ def cast_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
                                             _lib.stream_ptr()), "cast")
 
 
+def uncast_bf16(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """bf16 ``src`` -> fp32 ``dst`` (same numel) on the current stream."""
+    _lib.check(_lib.kernels().imk_uncast_bf16(src.data_ptr(), dst.data_ptr(), src.numel(),
+                                              _lib.stream_ptr()), "uncast")
+
+
 class TransposePlan:
     """Batched ``[Co][T][Ci] -> [Ci][T][Co]`` re-layout of every conv's bf16
     weight shadow into its dgrad shadow: one launch per optimizer step."""

@@ -28,6 +28,11 @@ MI355X design:
   the compute stream joins once at the end of backward. Bucket sizes target
   xGMI: a small first bucket (fc grads are ready first) and mid-size caps
   so several collectives overlap the remaining backward.
+* ``grad_reduce_dtype='bf16'``: each bucket is rounded into a bf16 copy, the
+  copy is all-reduced (half the xGMI bytes of the fp32 buckets; SURVEY §5.8
+  sizes the plan at bf16) and written back into the fp32 arena -- on the comm
+  stream for RCCL, so the casts overlap the backward like the collective. The
+  fp32 masters, momentum and SGD are unchanged.
 """
 
 from __future__ import annotations
@@ -135,7 +140,7 @@ class DataParallel(nn.Module):
                  bucket_cap_mb: float = 16.0, first_bucket_mb: float = 2.0,
                  broadcast_buffers: str = "eval", rebuild_buckets: bool = True,
                  find_unused_parameters: bool = False, use_autograd_hooks: Optional[bool] = None,
-                 probe_order: bool = False):
+                 probe_order: bool = False, grad_reduce_dtype: str = "fp32"):
         super().__init__()
         self.module = module
         self.arena = arena
@@ -154,6 +159,13 @@ class DataParallel(nn.Module):
         # the comm stream right after its all-reduce; see verify_order()
         self.probe_order = probe_order
         self._probe_sums: Optional[torch.Tensor] = None
+        if grad_reduce_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"grad_reduce_dtype must be fp32 or bf16, not {grad_reduce_dtype!r}")
+        self.grad_reduce_dtype = grad_reduce_dtype
+        # bf16 bucket copies: one buffer shaped like the arena (bucket b = the same slice)
+        self._g16 = (torch.empty(self.arena.G.numel(), dtype=torch.bfloat16, device=self.arena.G.device)
+                     if grad_reduce_dtype == "bf16" else None)
+        self._g16_pending: List[int] = []  # buckets to write back after join (no comm stream)
 
         self._verify_and_broadcast()
         self._plan()
@@ -283,9 +295,27 @@ class DataParallel(nn.Module):
             # bucket members may have been produced on the wgrad side stream:
             # the all-reduce waits for it too (main stream not blocked)
             self.comm.depend_on(side)
-        self.comm.allreduce_(self.arena.G[lo:hi], "avg")
+        if self._g16 is None:
+            self.comm.allreduce_(self.arena.G[lo:hi], "avg")
+        else:
+            self._launch_bf16(b, lo, hi)
         if self.probe_order:
             self._probe(b, lo, hi)
+
+    def _launch_bf16(self, b: int, lo: int, hi: int) -> None:
+        g, h = self.arena.G[lo:hi], self._g16[lo:hi]
+        s = getattr(self.comm, "stream", None) if g.is_cuda else None
+        if s is not None:
+            from ..ops.misc import cast_bf16, uncast_bf16
+            self.comm.depend_on(torch.cuda.current_stream(g.device))  # after the producers
+            with torch.cuda.stream(s):  # cast, reduce, write back: all ordered on the comm stream
+                cast_bf16(g, h)
+                self.comm.allreduce_(h, "avg")
+                uncast_bf16(h, g)
+        else:
+            h.copy_(g)
+            self.comm.allreduce_(h, "avg")
+            self._g16_pending.append(b)  # the collective may still be in flight: write back after join
 
     def _probe(self, b: int, lo: int, hi: int) -> None:
         s = getattr(self.comm, "stream", None)
@@ -339,6 +369,10 @@ class DataParallel(nn.Module):
                 self._launch(b)
         streams.join_side_into_current()  # the optimizer reads the gradient arena
         self.comm.join()
+        for b in self._g16_pending:
+            lo, hi, _ = self.buckets[b]
+            self.arena.G[lo:hi].copy_(self._g16[lo:hi])
+        self._g16_pending.clear()
         self.iteration += 1
         self.last_order = order
         if self.rebuild_pending and self.iteration == 1 and order:

@@ -317,7 +317,8 @@ class Trainer:
         self.comm = make_communicator(self.ctx, a.comm)
         self.ddp = DataParallel(model, arena, self.comm, bucket_cap_mb=a.bucket_mb,
                                 first_bucket_mb=a.first_bucket_mb, broadcast_buffers=a.broadcast_buffers,
-                                rebuild_buckets=a.rebuild_buckets)
+                                rebuild_buckets=a.rebuild_buckets,
+                                grad_reduce_dtype=getattr(a, "grad_allreduce_dtype", "fp32"))
         if self.native is not None:  # the rank-0 broadcast may have rewritten the fp32 masters
             self.native.refresh_shadows(full=True)
         after = self.native.refresh_shadows if self.native else None

@@ -131,3 +131,81 @@ def test_torch_override_without_process_group(monkeypatch):
     c.allreduce_(t, "avg")
     c.join()
     assert t.tolist() == [1.0] * 3
+
+
+class _FakeRcclOk:
+    """libimagent_comm stand-in where every rank's non-blocking init finishes after a few polls."""
+
+    def __init__(self, rank):
+        self.rank, self.uid, self.polls, self.aborted = rank, None, 0, False
+
+    def imc_unique_id_bytes(self):
+        return 128
+
+    def imc_get_unique_id(self, buf):
+        buf.raw = bytes(range(128))
+        return 0
+
+    def imc_comm_init_start(self, uid, n, rank, dev, nev, nb, out):
+        self.uid = bytes(uid)
+        out._obj.value = 0x2000 + rank
+        return 0
+
+    def imc_comm_set_stream_mode(self, h, mode):
+        return 0
+
+    def imc_comm_poll(self, h):
+        self.polls += 1
+        return 0 if self.polls >= 3 else 1  # "still initialising" twice, then ready
+
+    def imc_comm_stream(self, h):
+        return 0
+
+    def imc_comm_nranks(self, h):
+        return 2
+
+    def imc_async_error(self, h):
+        return 0
+
+    def imc_abort(self, h):
+        self.aborted = True
+        return 0
+
+    def imc_comm_destroy(self, h):
+        return 0
+
+    def imc_last_error(self):
+        return b""
+
+
+def _ok_worker(rank, port, outdir):
+    import os
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        from imagent_amd.ops import _lib
+        from imagent_amd.parallel import comm as C
+        fake = _FakeRcclOk(rank)
+        _lib.comm = lambda: fake
+        torch.cuda.ExternalStream = lambda ptr, device=None: SimpleNamespace(cuda_stream=ptr)  # no GPU here
+        ctx = SimpleNamespace(rank=rank, world_size=2, device=torch.device("cuda", 0))
+        c = C.make_communicator(ctx, "rccl")
+        assert c.name == "rccl" and isinstance(c, C.RcclCommunicator)
+        assert fake.uid == bytes(range(128)), "rank 0's unique id did not reach this rank"
+        assert fake.polls == 3 and not fake.aborted
+        assert c.nranks == 2 and c.healthy()
+        assert C.RcclCommunicator.live == 1
+        c.close()
+        assert C.RcclCommunicator.live == 0
+        open(os.path.join(outdir, f"ok{rank}"), "w").close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_bootstrap_success_on_all_ranks(tmp_path):
+    """The success path of the own-RCCL bootstrap (unique id through the c10d store, non-blocking init
+    polled to completion, the all-ranks agreement): every rank gets an RCCL communicator, none falls back
+    or aborts."""
+    import os
+    mp.start_processes(_ok_worker, args=(_free_port(), str(tmp_path)), nprocs=2, start_method="spawn", join=True)
+    assert os.path.exists(tmp_path / "ok0") and os.path.exists(tmp_path / "ok1")

@@ -120,3 +120,27 @@ def test_interrupted_val_sort_resumes_from_its_plan(tmp_path):
     got = {os.path.basename(p): y for p, y in ImageNetU8(str(tmp_path), "val", (6, 6)).samples}
     for k, g in enumerate(gt):
         assert got[f"ILSVRC2012_val_{k + 1:08d}.JPEG"] == g - 1
+
+
+def test_prepared_tree_on_read_only_root(tmp_path):
+    """a tree already in class-folder layout on a read-only mount (shared SLURM storage)
+    needs no lock file: prepare() returns before opening one, and the dataset constructs."""
+    pytest.importorskip("scipy")
+    from imagent_amd.data.devkit import prepare
+    from imagent_amd.data.imagenet import ImageNetU8
+    root = tmp_path / "ro"
+    root.mkdir()
+    _make(str(root))
+    for split in ("train", "val"):
+        prepare(str(root), split)
+    os.remove(root / ".imagent_prepare.lock")
+    os.chmod(root, 0o555)
+    try:
+        if os.access(root, os.W_OK):  # running as root: permissions do not bind, check the no-lock path directly
+            prepare(str(root), "val")
+            assert not os.path.exists(root / ".imagent_prepare.lock")
+        assert len(ImageNetU8(str(root), "val", (6, 6))) == 5
+        assert len(ImageNetU8(str(root), "train", (6, 6))) == 6
+        assert not os.path.exists(root / ".imagent_prepare.lock")
+    finally:
+        os.chmod(root, 0o755)

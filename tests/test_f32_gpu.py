@@ -99,7 +99,8 @@ def test_conv_f32_split(shape):
     assert rel(dw.permute(0, 3, 1, 2), w.grad) < TOL, rel(dw.permute(0, 3, 1, 2), w.grad)
 
 
-@pytest.mark.parametrize("C,res,relu", [(64, False, True), (128, True, True), (256, False, False), (512, True, True)])
+@pytest.mark.parametrize("C,res,relu", [(64, False, True), (128, True, True), (256, False, False), (512, True, True),
+                                        (1024, False, True), (2048, True, True)])
 def test_bn_f32(C, res, relu):
     from imagent_amd.models.resnet import BatchNorm2d
     from imagent_amd.ops.f32 import BNF32Fn, F32Workspace
@@ -203,6 +204,45 @@ def test_resnet18_f32_training_step_matches_torch(split):
         _r18_f32_steps(4e-2 if split else 1e-2, True)
     finally:
         set_split(False)
+
+
+def test_resnet50_f32_forward_backward_matches_float64():
+    """ResNet-50 on the fp32 kernels (2048-channel BatchNorms: two 1024-channel statistics slices):
+    one forward + backward on 4 images against the same model in float64. Loss within 1e-4;
+    gradients within 3x PyTorch fp32's own distance to float64 or 1e-2 (ReLU flips, see the ResNet-18
+    test)."""
+    import copy
+    from imagent_amd.data.loader import InputTransform
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native_f32 import bind_native_f32
+    from imagent_amd.ops.f32 import XentF32Fn
+    torch.manual_seed(5)
+    ref = resnet.resnet50(num_classes=100).to(DEV)
+    ref64 = copy.deepcopy(ref).double()
+    m = resnet.resnet50(num_classes=100)
+    m.load_state_dict(ref.state_dict())
+    st = bind_native_f32(m, DEV)
+    u8 = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8, device=DEV)
+    y = torch.randint(0, 100, (4,), device=DEV)
+    xr = InputTransform("torch", (64, 64))(u8)
+    xh = InputTransform("hip_f32", (64, 64), cpad=4)(u8)
+    for mm in (ref, ref64, m):
+        mm.train()
+    st.arena.zero_grad()
+    l32 = F.cross_entropy(ref(xr), y)
+    l32.backward()
+    l64 = F.cross_entropy(ref64(xr.double()), y)
+    l64.backward()
+    met = torch.zeros(4, device=DEV)
+    loss = XentF32Fn.apply(m(xh), y, met, 0.0)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - l64.item()) < 1e-4 * max(1.0, abs(l64.item())), (loss.item(), l64.item())
+    g32 = {n: p.grad for n, p in ref.named_parameters()}
+    g64 = {n: p.grad for n, p in ref64.named_parameters()}
+    bad = [(n, f"{rel(p.grad, g64[n]):.2e}", f"{rel(g32[n], g64[n]):.2e}") for n, p in m.named_parameters()
+           if not rel(p.grad, g64[n]) <= max(3 * rel(g32[n], g64[n]), 1e-2)]
+    assert not bad, bad
 
 
 def _r18_f32_steps(gfloor, resync):
