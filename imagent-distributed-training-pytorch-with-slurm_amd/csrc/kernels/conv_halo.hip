@@ -156,6 +156,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
     const int ec = lane & 7, ep0 = 32 * wid + (lane >> 3);
     const bool want_st = a.stats != nullptr;
     const bool accum = a.flags & IG_ACCUM;
+    const bool affine = a.flags & IG_AFFINE, relu = a.flags & IG_RELU;  // eval forward (EPI 0 only)
     const bool has_y = EPI == 1 && a.bnym != nullptr, has_x2 = EPI == 1 && a.bnx2 != nullptr;
     float c0[8], c1[8], c2[8], c3[8];  // per-channel constants (see below)
     float s1[8], s2[8], s3[8];
@@ -163,9 +164,11 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
     for (int k = 0; k < 8; ++k) {
         const int n = ec * 8 + k;
         s1[k] = s2[k] = s3[k] = 0.f;
-        if (EPI == 0) {  // c0 = shift
+        if (EPI == 0) {  // c0 = shift; c2 / c3 = the folded inference BatchNorm (IG_AFFINE: a.bias = [scale | shift])
             c0[k] = (want_st && a.shift) ? a.shift[n] : 0.f;
-            c1[k] = c2[k] = c3[k] = 0.f;
+            c1[k] = 0.f;
+            c2[k] = affine ? a.bias[n] : 1.f;
+            c3[k] = affine ? a.bias[a.Nout + n] : 0.f;
         } else {  // c0 = mean, c1 = rstd, c2/c3 = mask affine (from x) or second branch mean / rstd
             c0[k] = a.bnsave[n];
             c1[k] = a.bnsave[a.Nout + n];
@@ -248,6 +251,10 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
             u32x4 xw = {0u, 0u, 0u, 0u}, x2w = xw, ow = xw;
             uint32_t yw = 0u;
             if (accum) ow = *reinterpret_cast<const u32x4*>(yp);
+            if (EPI == 0 && affine) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = fmaf(v[q], c2[q], c3[q]);
+            }
             if (EPI == 1) {
                 xw = *reinterpret_cast<const u32x4*>(a.bnx + e);
                 if (has_y) yw = a.bnym[e >> 3];
@@ -286,6 +293,10 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                     if (has_x2) s3[q] += v[q] * ((x2v[q] - c2[q]) * c3[q]);
                 }
             } else {
+                if (relu) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+                }
                 u32x4 out;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) out[q] = pack_bf2(v[2 * q], v[2 * q + 1]);
@@ -367,8 +378,11 @@ int conv_halo(const IGemmArgs& a, hipStream_t st) {
         return !e || e[0] != '0';
     }();
     if (!on) return 1;
-    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_REGSTAGE | IG_FP8 | IG_AFFINE | IG_ACCUM_SUB2)) return 1;
-    if (a.bias || a.C != 64 || a.Nout != 64 || a.ldb < 9 * 64 || a.ldy != 64) return 1;
+    if (a.flags & (IG_OUT_F32 | IG_STEM | IG_REGSTAGE | IG_FP8 | IG_ACCUM_SUB2)) return 1;
+    // the eval forward's folded BatchNorm (+ ReLU after the optional accumulate): plain epilogue only
+    if ((a.flags & (IG_AFFINE | IG_RELU)) && ((a.flags & IG_BNBWD) || a.stats || a.xbn)) return 1;
+    if ((a.flags & IG_RELU) && !(a.flags & IG_AFFINE)) return 1;
+    if ((a.bias && !(a.flags & IG_AFFINE)) || a.C != 64 || a.Nout != 64 || a.ldb < 9 * 64 || a.ldy != 64) return 1;
     if (a.nth != 3 || a.ntw != 3 || a.KW != 3 || a.sA != 1 || a.sY != 1 || a.oy != 0 || a.ox != 0) return 1;
     if (a.OH != a.H || a.OW != a.W || a.YH != a.H || a.YW != a.W) return 1;
     if (!tap_in_halo(a.dh0, a.dhs) || !tap_in_halo(a.dw0, a.dws)) return 1;

@@ -167,7 +167,10 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         if (t8 >= 192) tile = 8;
     }
     const bool bnb = a.flags & IG_BNBWD;
-    const bool lds_ok = !(a.flags & (IG_OUT_F32 | IG_RELU)) && !a.bias && a.Nout % 8 == 0 && a.ldy % 8 == 0;
+    // staged epilogue: bf16, no bias; the eval forward's folded BatchNorm (+ ReLU) too
+    const bool eval_bn = (a.flags & IG_AFFINE) && !a.stats;
+    const bool lds_ok = !(a.flags & IG_OUT_F32) && (!(a.flags & IG_RELU) || eval_bn) && (!a.bias || eval_bn) &&
+                        a.Nout % 8 == 0 && a.ldy % 8 == 0;
     // staged epilogue: always with the fused BN backward; otherwise for long-K
     // tiles (non-persistent anyway, +5-10 % measured) -- short-K memory-bound
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap

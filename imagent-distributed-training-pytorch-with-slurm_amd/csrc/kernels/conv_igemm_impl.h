@@ -431,6 +431,9 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
     const int n = n0 + cc * 8;
     const bool nok = n < a.Nout;  // Nout % 8 == 0 on this path
     float mean[8], rstd[8], sc[8], sh[8], m2[8], r2[8];
+    // plain epilogue: the eval forward's folded BatchNorm (IG_AFFINE: a.bias = [scale | shift] -> sc / sh),
+    // applied to the bf16-rounded conv output as the training BatchNorm is, then the accumulate, then ReLU
+    const bool affine = !bnb && (a.flags & IG_AFFINE), relu = !bnb && (a.flags & IG_RELU);
     if (!bnb) {  // forward statistics: mean[] holds the shift (previous batch mean, or 0)
         const bool ld = st && a.shift && nok;
         const f32x4 lo = ld ? *reinterpret_cast<const f32x4*>(a.shift + n) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -439,6 +442,18 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
         for (int c = 0; c < 4; ++c) {
             mean[c] = lo[c];
             mean[4 + c] = hi[c];
+        }
+        const bool la = affine && nok;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 s4 = la ? *reinterpret_cast<const f32x4*>(a.bias + n + 4 * h) : f32x4{1.f, 1.f, 1.f, 1.f};
+            const f32x4 t4 =
+                la ? *reinterpret_cast<const f32x4*>(a.bias + a.Nout + n + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                sc[4 * h + c] = s4[c];
+                sh[4 * h + c] = t4[c];
+            }
         }
     }
     // (1) fragments -> LDS
@@ -516,9 +531,17 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
             for (int k = 0; k < 4; ++k) {
                 v[2 * k] = lo_bf(t[k]);
                 v[2 * k + 1] = hi_bf(t[k]);
+                if (affine) {
+                    v[2 * k] = fmaf(v[2 * k], sc[2 * k], sh[2 * k]);
+                    v[2 * k + 1] = fmaf(v[2 * k + 1], sc[2 * k + 1], sh[2 * k + 1]);
+                }
                 if (accum) {
                     v[2 * k] += lo_bf(oo[u][k]);
                     v[2 * k + 1] += hi_bf(oo[u][k]);
+                }
+                if (relu) {
+                    v[2 * k] = fmaxf(v[2 * k], 0.f);
+                    v[2 * k + 1] = fmaxf(v[2 * k + 1], 0.f);
                 }
             }
             float xv[8];

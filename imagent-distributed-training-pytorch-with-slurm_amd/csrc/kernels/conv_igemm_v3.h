@@ -221,11 +221,14 @@ int launch_v3(const IGemmArgs& a, hipStream_t st) {
 }
 
 // shapes v3 covers: C % 64 == 0 (one tap per stage), taps <= 32, operands < 2^31 bytes, and the staged
-// (bf16, no bias / ReLU) epilogue
+// bf16 epilogue (no bias; ReLU only with the eval forward's folded BatchNorm, IG_AFFINE, without statistics)
 inline bool v3_ok(const IGemmArgs& a) {
     if (a.C % 64 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
-    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_STEM | IG_FP8 | IG_AFFINE)) return false;
-    if (a.bias || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
+    if (a.flags & (IG_OUT_F32 | IG_STEM | IG_FP8)) return false;
+    const bool eval_bn = a.flags & IG_AFFINE;
+    if ((a.flags & IG_RELU) && !eval_bn) return false;
+    if (eval_bn && (a.stats || (a.flags & IG_BNBWD))) return false;
+    if ((a.bias && !eval_bn) || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
     const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
     return xb < (1ull << 31) && wb < (1ull << 31);
 }

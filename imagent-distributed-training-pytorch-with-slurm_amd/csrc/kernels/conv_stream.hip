@@ -107,9 +107,16 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
         }
     }
-    if (!bnb) {  // forward statistics: mean[] holds the shift (previous batch mean, or 0)
+    // plain epilogue: forward statistics (mean[] holds the shift: previous batch mean, or 0) and the eval
+    // forward's folded BatchNorm (IG_AFFINE: a.bias = [scale | shift] -> sc / sh) + ReLU after the accumulate
+    const bool affine = !bnb && (a.flags & IG_AFFINE), relu = !bnb && (a.flags & IG_RELU);
+    if (!bnb) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) mean[c] = (a.stats && a.shift) ? a.shift[n + c] : 0.f;
+        for (int c = 0; c < 8; ++c) {
+            mean[c] = (a.stats && a.shift) ? a.shift[n + c] : 0.f;
+            sc[c] = affine ? a.bias[n + c] : 1.f;
+            sh[c] = affine ? a.bias[a.Nout + n + c] : 0.f;
+        }
     }
     float s1[8], s2[8], s3[8];
 #pragma unroll
@@ -273,9 +280,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     for (int k = 0; k < 4; ++k) {
                         v[2 * k] = lo_bf(t[k]);
                         v[2 * k + 1] = hi_bf(t[k]);
+                        if (affine) {
+                            v[2 * k] = fmaf(v[2 * k], sc[2 * k], sh[2 * k]);
+                            v[2 * k + 1] = fmaf(v[2 * k + 1], sc[2 * k + 1], sh[2 * k + 1]);
+                        }
                         if (accum) {
                             v[2 * k] += lo_bf(oo[q][k]);
                             v[2 * k + 1] += hi_bf(oo[q][k]);
+                        }
+                        if (relu) {
+                            v[2 * k] = fmaxf(v[2 * k], 0.f);
+                            v[2 * k + 1] = fmaxf(v[2 * k + 1], 0.f);
                         }
                     }
                     float xv[8];
@@ -380,14 +395,19 @@ int launch_stream(const IGemmArgs& a, hipStream_t st) {
 // Returns 1 if the shape is not one this kernel covers (caller falls back).
 // bn: channel-slice width (0 auto: the widest that divides Nout; 64/128/256 forced)
 int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
+    // the eval forward's folded BatchNorm (+ ReLU): plain epilogue, no statistics
+    const bool eval_bn = a.flags & IG_AFFINE;
+    if ((a.flags & IG_RELU) && !eval_bn) return 1;
+    if (eval_bn && (a.stats || a.xbn || (a.flags & IG_BNBWD))) return 1;
+    const bool has_bias = a.bias && !eval_bn;
     if (a.flags & IG_STEM) {  // 7x7 stem, C = 4, K = 7 x 32
-        if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_ACCUM | IG_BNBWD | IG_NOSTREAM)) return 1;
-        if (a.bias || a.C != 4 || a.nth != 7 || a.ntw > 8 || a.ldb != 7 * 32 || a.Nout % 64 || a.ldy != a.Nout ||
+        if (a.flags & (IG_OUT_F32 | IG_FP8 | IG_ACCUM | IG_BNBWD | IG_NOSTREAM)) return 1;
+        if (has_bias || a.C != 4 || a.nth != 7 || a.ntw > 8 || a.ldb != 7 * 32 || a.Nout % 64 || a.ldy != a.Nout ||
             a.sY != 1 || a.YH != a.OH || a.YW != a.OW)
             return 1;
         return launch_stream1<7 * 32, 64, 2, 0, true>(a, st);
     }
-    if (a.flags & (IG_OUT_F32 | IG_RELU | IG_FP8 | IG_AFFINE | IG_REGSTAGE | IG_NOSTREAM)) return 1;
+    if (a.flags & (IG_OUT_F32 | IG_FP8 | IG_REGSTAGE | IG_NOSTREAM)) return 1;
     if (a.xbn) {  // BN apply + ReLU on the operand load: K = 64 / 128 plain-epilogue 1x1 convs only
         if ((a.flags & (IG_BNBWD | IG_ACCUM)) || a.bias || a.nth != 1 || a.ntw != 1 || a.sA != 1 ||
             a.H != a.OH || a.W != a.OW || a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout ||
@@ -398,7 +418,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         if (a.C == 128 && a.Nout % 128 == 0) return launch_stream1<128, 128, 2, 0, false, true>(a, st);
         return -120;
     }
-    if (a.bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
+    if (has_bias || a.nth != 1 || a.ntw != 1 || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0) return 1;
     if (a.sY != 1 || a.oy != 0 || a.ox != 0 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout) return 1;
     if (a.Nout % 64 != 0 || a.ldb < a.C) return 1;
     if ((long)(a.OH - 1) * a.sA >= a.H || (long)(a.OW - 1) * a.sA >= a.W) return 1;

@@ -419,3 +419,47 @@ def test_fused_stem_pool_backward_matches_unfused():
     assert rel(g1, g0) < 5e-3
     assert rel(w1, w0) < 1e-3
     assert rel(b1, b0) < 1e-3
+
+
+@pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
+def test_eval_forward_224_matches_torch(arch):
+    """The eval forward (every BatchNorm + ReLU folded into its conv's epilogue, the block's last conv
+    accumulating onto the shortcut) at 224x224, where it runs the training kernels' families with
+    the IG_AFFINE epilogue: the halo 3x3 at 56x56, the streaming 1x1 convs and stem, and the v3
+    staged epilogue. Non-trivial running statistics and
+    affine parameters; logits against the fp32 PyTorch model within 2x the bf16-autocast oracle's
+    distance (or 5e-2)."""
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native import bind_native
+    from imagent_amd.ops.misc import normalize_u8
+    torch.manual_seed(4)
+    ref = resnet.build(arch, num_classes=1000).to(DEV)
+    with torch.no_grad():
+        for m in ref.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    model = copy.deepcopy(ref)
+    bind_native(model, DEV)
+    with torch.no_grad():
+        for p_ref, p in zip(ref.parameters(), model.parameters()):
+            p_ref.copy_(p.to(torch.bfloat16).float())
+    B, H = 4, 224
+    low = torch.rand(B, 3, 16, 16, device=DEV)
+    img = (F.interpolate(low, size=(H, H), mode="bicubic", align_corners=False).clamp(0, 1) * 255)
+    img = img.to(torch.uint8).permute(0, 2, 3, 1).contiguous()
+    x = normalize_u8(img, (H, H), 4, (0.5,) * 3, (0.5,) * 3)
+    xr = x[..., :3].float().permute(0, 3, 1, 2).contiguous()
+    model.eval()
+    ref.eval()
+    with torch.no_grad():
+        r32 = ref(xr)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ebf = rel(ref(xr).float(), r32)
+        got = model(x).float()
+        torch.cuda.synchronize()
+    e = rel(got, r32)
+    print(f"{arch} eval logits: hip {e:.4f} autocast-bf16 {ebf:.4f}")
+    assert e < max(5e-2, 2.0 * ebf), (e, ebf)
