@@ -126,13 +126,19 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     const float* __restrict__ gamma2, const float* __restrict__ beta2, bf16_t* __restrict__ y,
     float* __restrict__ save, float* __restrict__ save2, long R, int C, float inv_cnt, float eps,
     int eval, uint32_t* __restrict__ y8, const int* __restrict__ exp8, float* __restrict__ amax8,
-    uint8_t* __restrict__ ym) {
+    uint8_t* __restrict__ ym, float* __restrict__ colsum) {
     const int cpr = C / 8;                // chunks per row
     const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
     const int tid = threadIdx.x;
     // fp8 copy of the output for the next conv (delayed-scaled e4m3, fp8.hip)
     const float q8 = Q8 ? ldexpf(1.f, -exp8[0]) : 0.f;
     float m8 = 0.f;
+    // colsum (mode 0): column sums of the stored (bf16) output -- the Gram-form bn3 backward's 1^T h2
+    // (bn_gram.hip) -- per thread over its rows, folded over the block's row groups, one atomic per
+    // channel per block (host: C / 8 divides 256, every lane active)
+    float cs[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cs[i] = 0.f;
     if (tid >= rpb * cpr) return;  // (host: with y8, every lane is active -- C/8 divides 256)
     const int ch = tid % cpr, c0 = ch * 8;
     float sc[8], sh[8], sc2[8], sh2[8];
@@ -189,6 +195,10 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) pw[i] = pack_bf2(o8[2 * i], o8[2 * i + 1]);
             stw<NT>(y + (size_t)r * C + c0, pw);
+            if (MODE == 0 && colsum) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) cs[i] += bfw(pw, i);
+            }
             if (MODE != 0 && RELU && ym) {  // the ReLU mask as bits for the backward's dgrad epilogue
                 uint32_t b = 0;
 #pragma unroll
@@ -210,6 +220,18 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
                     u32x2{pack4_fp8(w[0] * q8, w[1] * q8, w[2] * q8, w[3] * q8),
                           pack4_fp8(w[4] * q8, w[5] * q8, w[6] * q8, w[7] * q8)};
             }
+        }
+    }
+    if (MODE == 0 && colsum) {
+        __shared__ float red[256][9];  // [thread][channel of its chunk] (+1: bank spread)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[tid][i] = cs[i];
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            const int cc = c / 8, i = c % 8;
+            float t = 0.f;
+            for (int g = 0; g < rpb; ++g) t += red[g * cpr + cc][i];
+            atomicAdd(colsum + c, t);
         }
     }
     if (Q8) {  // every lane active (host check): block max, one atomic per block into a 32-slot amax row
@@ -677,9 +699,10 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
                           const void* x2, const float* sums2, const float* gamma2, const float* beta2,
                           void* y, float* save, float* save2, long R, int C, int mode, int relu,
                           float eps, int eval, void* y8, const int* exp8, float* amax8, void* ym,
-                          void* stream) {
+                          float* colsum, void* stream) {
     if (C % 8 || C > 2048) return -100;
     if (y8 && (256 % (C / 8) || !exp8 || !amax8)) return -102;
+    if (colsum && (mode != 0 || 256 % (C / 8))) return -103;
     const float inv_cnt = 1.f / (float)R;
     const int grid = grid_for(R, C);
     hipStream_t st = (hipStream_t)stream;
@@ -688,7 +711,7 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
     hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>),                                                  \
                        dim3(resident_grid((const void*)bn_fwd_kernel<M, RL, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)x, sums, \
                        gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, R, C,   \
-                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym)
+                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym, colsum)
 #define L(M, RL)                                              \
     do {                                                      \
         if (q8) { if (nt) LK(M, RL, true, true); else LK(M, RL, false, true); }   \

@@ -1,0 +1,120 @@
+// BatchNorm backward of a bottleneck's last BatchNorm (bn3) without its apply pass, gfx950.
+//
+// The reference trains torchvision's Bottleneck (imagenet.py:312; backward :128):
+//     x3 = conv3(h2)  (1x1, p -> 4p channels),  y = relu(bn3(x3) + identity)
+// Its BatchNorm backward is, per output channel o (bn_bwd_apply_kernel, bn.hip),
+//     dx3 = A_o g + B_o x3 + c_o,   A = gamma rstd,  B = -gamma rstd^2 mean(g xhat),
+//                                   c = -gamma rstd mean(g) - B mean
+// for the ReLU-masked upstream gradient g (its reductions come from the producing dgrad's epilogue).
+// dx3 is 4p channels wide -- the widest activation of the block -- and the apply pass that writes
+// it (read g, x3; write dx3) was the largest BatchNorm cost of the step. Both consumers of dx3 are
+// linear in it, and x3 = h2 W3^T, so the x3 term folds into p x p matrices:
+//   dgrad:  dh2 = dx3 W3 = g (diag(A) W3) + h2 (W3^T diag(B) W3) + c W3
+//           -> ONE GEMM over K = [g | h2] (4p + p instead of 4p: +25 % MACs) with the weights
+//              Wcat[i] = [A_o W3[o][i] | Q[j][i]], Q = W3^T diag(B) W3, and the bias c W3;
+//   wgrad:  dW3 = dx3^T h2 = diag(A) (g^T h2) + diag(B) W3 (h2^T h2) + c (1^T h2)
+//           -> the weight-gradient GEMM of g, the p x p Gram matrix G = h2^T h2 (+25 %), the
+//              column sums of h2, and an elementwise fix-up (bn_gram_wgrad_fixup_kernel).
+// (x3 enters as h2 W3^T in full precision instead of its bf16-rounded copy: a 2^-9 relative
+// difference inside the B term.) ops/block.py drives it; tests/test_model_gpu.py holds it to the
+// fp32 PyTorch model.
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int BWD_SLOTS_G = 32;  // the BN-backward reduction slab slots (bn.hip BWD_SLOTS, STAT_SLOTS)
+
+// coef [3][C] = (A, B, c) from the dgrad epilogue's slab [S][3][C] (sum g xhat, sum g, -);
+// dgamma / dbeta accumulate as in the apply pass (slot order as stats_finalize_kernel)
+__global__ void bn_bwd_coef_kernel(const float* __restrict__ slab, const float* __restrict__ save,
+                                   const float* __restrict__ gamma, float* __restrict__ dgamma,
+                                   float* __restrict__ dbeta, float* __restrict__ coef, int S, int C,
+                                   float inv_cnt) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float sgx = 0.f, sg = 0.f;
+    for (int s = 0; s < S; ++s) {
+        sgx += slab[(size_t)s * 3 * C + c];
+        sg += slab[(size_t)s * 3 * C + C + c];
+    }
+    if (dgamma) dgamma[c] += sgx;
+    if (dbeta) dbeta[c] += sg;
+    const float mean = save[c], rstd = save[C + c], gr = gamma[c] * rstd;
+    const float k0 = -gr * inv_cnt * sg, kx = -gr * inv_cnt * sgx * rstd;
+    coef[c] = gr;
+    coef[C + c] = kx;
+    coef[2 * C + c] = k0 - kx * mean;
+}
+
+// dgrad weights: wt [p][ldw] bf16 = W3^T (row i: input channel i of conv3, columns o < C4),
+// Q [p][p] fp32 -> wcat [p][C4 + p] bf16 = [A_o wt[i][o] | Q[i][j]], bias [p] = sum_o c_o wt[i][o]
+__global__ __launch_bounds__(256) void bn_gram_dgrad_weights_kernel(const bf16_t* __restrict__ wt, int ldw,
+                                                                    const float* __restrict__ coef,
+                                                                    const float* __restrict__ Q,
+                                                                    bf16_t* __restrict__ wcat,
+                                                                    float* __restrict__ bias, int p, int C4) {
+    const int i = blockIdx.x;
+    const int ld = C4 + p;
+    float part = 0.f;
+    for (int o = threadIdx.x; o < C4; o += 256) {
+        const float w = bf2f(wt[(size_t)i * ldw + o]);
+        wcat[(size_t)i * ld + o] = f2bf(w * coef[o]);
+        part += w * coef[2 * C4 + o];
+    }
+    for (int j = threadIdx.x; j < p; j += 256) wcat[(size_t)i * ld + C4 + j] = f2bf(Q[(size_t)i * p + j]);
+    __shared__ float red[256];
+    red[threadIdx.x] = part;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bias[i] = red[0];
+}
+
+// dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + c_o s[i]   (T = g^T h2, P = W3 G, s = colsum h2)
+__global__ __launch_bounds__(256) void bn_gram_wgrad_fixup_kernel(float* __restrict__ dw,
+                                                                  const float* __restrict__ T,
+                                                                  const float* __restrict__ P,
+                                                                  const float* __restrict__ coef,
+                                                                  const float* __restrict__ s, int C4, int p) {
+    const long n = (long)C4 * p;
+    for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+        const int o = (int)(e / p), i = (int)(e - (long)o * p);
+        dw[e] += fmaf(coef[o], T[e], fmaf(coef[C4 + o], P[e], coef[2 * C4 + o] * s[i]));
+    }
+}
+
+}  // namespace
+
+IMK_EXPORT int imk_bn_bwd_coef(const float* scratch, const float* save, const float* gamma, float* dgamma_acc,
+                               float* dbeta_acc, float* coef, long R, int C, void* stream) {
+    if (R <= 0 || C <= 0) return -100;
+    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, scratch, save,
+                       gamma, dgamma_acc, dbeta_acc, coef, BWD_SLOTS_G, C, 1.f / (float)R);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_gram_dgrad_weights(const void* wt, int ldw, const float* coef, const float* Q, void* wcat,
+                                         float* bias, int p, int C4, void* stream) {
+    if (p <= 0 || C4 <= 0 || ldw < C4) return -100;
+    hipLaunchKernelGGL(bn_gram_dgrad_weights_kernel, dim3(p), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)wt, ldw, coef, Q, (bf16_t*)wcat, bias, p, C4);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_gram_wgrad_fixup(float* dw, const float* T, const float* P, const float* coef, const float* s,
+                                       int C4, int p, void* stream) {
+    if (p <= 0 || C4 <= 0) return -100;
+    const long n = (long)C4 * p;
+    const int grid = (int)std::min<long>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(bn_gram_wgrad_fixup_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dw, T, P, coef, s,
+                       C4, p);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}

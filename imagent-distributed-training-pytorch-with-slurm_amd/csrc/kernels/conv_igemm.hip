@@ -125,6 +125,13 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
         return conv_stream(a, st);
     }
+    if (a.X2) {  // two K segments (bn_gram.hip): the v3 loop only
+        if (!v3_ok(a) || a.Nout % 64) return -106;
+        const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+        if (a.Nout >= 512 && t8 >= 192) return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+        if (a.Nout == 64) return launch_v3<128, 64, 1, 2, 4, 128>(a, st);
+        return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
+    }
     if (a.flags & IG_FP8) return conv_igemm_fp8(a, tile, st);
     if (a.C % 8 != 0) return -100;  // 16-byte chunks must not straddle taps
     if (tile == 0 && a.C == 64 && a.Nout == 64 && a.nth == 3 && a.ntw == 3) {

@@ -92,6 +92,11 @@ struct IGemmArgs {
     // the producing BatchNorm's apply + ReLU done on the consumer's operand load (ops/block.py),
     // so the BN output is never written
     const float* xbn;
+    // v3 only: a second K segment -- after the C channels of X, C2 more from X2 (same pixels, row pitch C2;
+    // 1x1 stride-1 gathers), the weights' columns [C, C + C2). With IG_BNBWD, `bias` [Nout] is added to
+    // the sums before the mask (bn_gram.hip: the bottleneck's bn3 backward folded into conv3's dgrad)
+    const bf16_t* X2;
+    int C2;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
@@ -460,6 +465,17 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
     put(smem, P);
     __syncthreads();
     // (2) row chunks: thread -> fixed channel chunk cc, rows rg + RG*q
+    float bb[8];  // IG_BNBWD: per-channel bias added before the mask (second K segment, bn_gram.hip)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bb[c] = 0.f;
+    if (bnb && nok && a.bias) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + n + 4 * h);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bb[4 * h + c] = b4[c];
+        }
+    }
     if (bnb && nok) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -529,8 +545,8 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
             float v[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                v[2 * k] = lo_bf(t[k]);
-                v[2 * k + 1] = hi_bf(t[k]);
+                v[2 * k] = lo_bf(t[k]) + bb[2 * k];
+                v[2 * k + 1] = hi_bf(t[k]) + bb[2 * k + 1];
                 if (affine) {
                     v[2 * k] = fmaf(v[2 * k], sc[2 * k], sh[2 * k]);
                     v[2 * k + 1] = fmaf(v[2 * k + 1], sc[2 * k + 1], sh[2 * k + 1]);

@@ -69,12 +69,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     const int m0 = (lid / nbn) * BM, n0 = (lid % nbn) * BN;
     const int ntaps = a.nth * a.ntw;
     const int cps = a.C / KS;          // stages per tap (C % 64 == 0, host)
-    const int nk = ntaps * cps;
+    const int nk1 = ntaps * cps;       // stages of the first K segment
+    const int nk = nk1 + (a.X2 ? a.C2 / KS : 0);  // + the second (X2: one tap, C2 % 64 == 0, host)
     const int ohw = a.OH * a.OW;
     const int lrow = lane / CPR;
     const int lchunk = (lane % CPR) ^ lds_swz<RB>(lrow);
     const __amdgpu_buffer_rsrc_t rx = v3_rsrc(a.X, (uint32_t)((size_t)a.N * a.H * a.W * a.C * 2));
     const __amdgpu_buffer_rsrc_t rw = v3_rsrc(a.Wk, (uint32_t)((size_t)a.Nout * a.ldb * 2));
+    const __amdgpu_buffer_rsrc_t rx2 =
+        v3_rsrc(a.X2 ? a.X2 : a.X, a.X2 ? (uint32_t)((size_t)a.M * a.C2 * 2) : 0u);
 
     // per X piece: byte offset of (img, ih0, iw0, lchunk) -- may be "negative" (a border pixel's
     // first tap), only valid taps' offsets are ever used -- and the valid-tap bit mask
@@ -98,6 +101,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
             }
         }
         xmask[q] = mk;
+    }
+    uint32_t xbase2[QA];  // second K segment: pixel row m of X2 (pitch C2), out-of-range rows read zeros
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+        const int m = m0 + (wid * QA + q) * RPP + lrow;
+        xbase2[q] = m < a.M ? (uint32_t)((size_t)m * a.C2 * 2 + lchunk * 16) : OOB_OFF;
     }
     uint32_t vw[QB];
 #pragma unroll
@@ -123,6 +132,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
         const int buf = is % NS;
         char* dX = sX + buf * SAB + (wid * QA) * 1024;
         char* dW = sW + buf * SBB + (wid * QB) * 1024;
+        if (is >= nk1) {  // second K segment (one tap): X2 rows, weight columns C + (is - nk1) * KS
+            const uint32_t so = (uint32_t)((is - nk1) * RB);
+#pragma unroll
+            for (int q = 0; q < QA; ++q) v3_dma(rx2, dX + q * 1024, xbase2[q], so);
+#pragma unroll
+            for (int q = 0; q < QB; ++q) v3_dma(rw, dW + q * 1024, vw[q], (uint32_t)(a.C * 2) + so);
+            ++is;
+            return;
+        }
         const uint32_t cso = (uint32_t)(ics * RB);
 #pragma unroll
         for (int q = 0; q < QA; ++q) v3_dma(rx, dX + q * 1024, vx[q], cso);
@@ -228,7 +246,11 @@ inline bool v3_ok(const IGemmArgs& a) {
     const bool eval_bn = a.flags & IG_AFFINE;
     if ((a.flags & IG_RELU) && !eval_bn) return false;
     if (eval_bn && (a.stats || (a.flags & IG_BNBWD))) return false;
-    if ((a.bias && !eval_bn) || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
+    const bool bnb_bias = (a.flags & IG_BNBWD) && a.X2;  // the second segment's bias (bn_gram.hip)
+    if ((a.bias && !eval_bn && !bnb_bias) || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
+    if (a.X2 && (a.C2 % 64 || a.C2 <= 0 || a.nth != 1 || a.ntw != 1 || a.sA != 1 || a.H != a.OH || a.W != a.OW ||
+                 a.ldb < a.C + a.C2 || (size_t)a.M * a.C2 * 2 >= (1ull << 31)))
+        return false;
     const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
     return xb < (1ull << 31) && wb < (1ull << 31);
 }

@@ -950,7 +950,7 @@ int sgrid(long work) {
 }
 
 int bn_blocks(long R, int C) {
-    const int rpb = 256 / (C / 4);
+    const int rpb = 256 / ((C < 1024 ? C : 1024) / 4);  // rows per block of one channel slice (bn_partial_f32)
     long b = (R + 4L * rpb - 1) / (4L * rpb);  // >= 4 rows per thread
     return (int)(b < BN_MAXB ? (b > 0 ? b : 1) : BN_MAXB);
 }

@@ -88,6 +88,7 @@ class IGemmArgs(C.Structure):
         ("bnbeta", C.c_void_p), ("bnx2", C.c_void_p), ("bnsave2", C.c_void_p),
         ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p),
         ("xbn", C.c_void_p),
+        ("X2", C.c_void_p), ("C2", C.c_int),
     ]
 
 
@@ -160,7 +161,7 @@ def _declare(name: str, lib) -> None:
             "imk_normalize_u8_f32": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_xent_bwd_f32": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
-                           vp, vp],
+                           vp, vp, vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
             "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
             "imk_bn_running_update": [vp, i32, vp],
@@ -180,6 +181,9 @@ def _declare(name: str, lib) -> None:
             "imk_xent_fwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_xent_bwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_colsum_bf16": [vp, vp, i32, i32, vp],
+            "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
+            "imk_bn_gram_dgrad_weights": [vp, i32, vp, vp, vp, vp, i32, i32, vp],
+            "imk_bn_gram_wgrad_fixup": [vp, vp, vp, vp, vp, i32, i32, vp],
             "imk_sgd": [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, f32, vp],
             "imk_cast_bf16": [vp, vp, i64, vp],
             "imk_uncast_bf16": [vp, vp, i64, vp],

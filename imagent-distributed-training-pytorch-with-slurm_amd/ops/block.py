@@ -33,6 +33,7 @@ import torch
 from . import streams
 from . import conv as _conv
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_scale_shift
+from .bn_gram import GramBN, gram_coef, gram_dgrad, gram_wgrad
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
@@ -57,6 +58,22 @@ _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 _XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "1") != "0"
 _XFUSE_3X3 = os.environ.get("IMAGENT_BN_XFUSE", "1") == "all"
 _HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
+# IMAGENT_BN_GRAM (default 1; 0 = A/B off): a bottleneck's last BatchNorm backward without its apply pass
+# (ops/bn_gram.py): conv3's dgrad runs over [g | h2] with folded weights, its wgrad from g^T h2 and the
+# Gram matrix of h2. conv3's input h2 is then kept (no operand-path BN fusion for that conv).
+_GRAM = os.environ.get("IMAGENT_BN_GRAM", "1") != "0"
+
+
+def _gram_ok(block, q, x) -> bool:
+    """Does this block's backward take bn3 through the Gram form (forward keeps h2)?"""
+    pairs = block.convs_bns()
+    if not (_GRAM and q is None and x.is_cuda and len(pairs) == 3 and block.downsample is None):
+        return False
+    if not getattr(block, "_fuse_bnb", False):  # the next block's dgrad must reduce bn3 (premasked backward)
+        return False
+    c3 = pairs[-1][0]
+    return (c3.kh == 1 and c3.kw == 1 and c3.stride == 1 and c3.padding == 0 and c3.in_channels % 64 == 0
+            and c3.out_channels % 64 == 0)
 
 
 def _xfuse_ok(conv, a, q) -> bool:
@@ -128,18 +145,22 @@ class BlockFn(torch.autograd.Function):
             with torch.cuda.stream(side):
                 ad = _fwd8(ds[0], x, x8, ds[1])
         xbn = [None] * len(pairs)  # xbn[i]: conv i applies the preceding BN + ReLU on its operand load
+        gram = _gram_ok(block, q, x)  # bn3 backward in the Gram form: conv3's input must exist
         ss = None
+        h2sum = None  # Gram form: colsum(h2), accumulated by the BN pass that writes h2
         for i, (conv, bn, _) in enumerate(pairs[:-1]):
             a = _fwd8(conv, h, h8, bn) if ss is None else \
                 igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
             ss = None
-            if _xfuse_ok(pairs[i + 1][0], a, q):
+            if not (gram and i + 1 == len(pairs) - 1) and _xfuse_ok(pairs[i + 1][0], a, q):
                 ss = xbn[i + 1] = bn_scale_shift(a, bn)
                 h, h8 = a, None
                 saved += [a, None]
                 continue
             q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
-            h = bn_act_forward(a, None, bn, None, 0, True, q8=q8)
+            if gram and i + 1 == len(pairs) - 1:
+                h2sum = torch.zeros(a.shape[-1], device=a.device, dtype=torch.float32)
+            h = bn_act_forward(a, None, bn, None, 0, True, q8=q8, colsum=h2sum)
             h8 = (q8[0], q8[1]) if q8 is not None else None
             saved += [a, h]
         conv, bn, _ = pairs[-1]
@@ -176,6 +197,8 @@ class BlockFn(torch.autograd.Function):
         block._bnb_done = False
         ctx.block = block
         ctx.xbn = xbn
+        ctx.gram = gram
+        ctx.h2sum = h2sum
         ctx.save_for_backward(*saved)
         return out
 
@@ -218,6 +241,9 @@ class BlockFn(torch.autograd.Function):
             dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw,
                              fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
+        elif premasked and ctx.gram and fuse:
+            dA = gram_coef(bn_l, dout)  # dx3 kept as (g, A, B, c): no apply pass (ops/bn_gram.py)
+            dX = dout
         elif premasked:
             g8a = q.grad_out(a_last, bn_l) if q is not None else None
             dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
@@ -229,17 +255,22 @@ class BlockFn(torch.autograd.Function):
         block._last_bn = None
         block._bnb_done = False
         xbn = ctx.xbn  # xbn[i]: conv i's input is BN(acts[i - 1]) + ReLU applied on its operand path
+        g_read = None  # side-stream event after the Gram wgrad's last read of dout (= dX)
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             h_in = inputs[i]
             if i > 0:
                 bn_prev = pairs[i - 1][1]
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
-                dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
-                                 conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
+                if isinstance(dA, GramBN):
+                    dH = gram_dgrad(dA, conv, h_in, fz)
+                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum)  # issued now: it reads dout, which conv1's dgrad
+                else:                                    # accumulates into below
+                    dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
+                                     conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
                 if h_in is None:  # xfuse: the weight gradient applies the BN on its operand staging
                     h_in = (acts[i - 1], xbn[i])
-                if not _DEFER_WGRAD:
+                if not _DEFER_WGRAD and not isinstance(dA, GramBN):
                     _wgrad(conv, dA, h_in)
                 dA_w = dA
                 if fz is not None:
@@ -249,7 +280,7 @@ class BlockFn(torch.autograd.Function):
                 else:
                     dA, _ = bn_act_backward(dH, acts[i - 1], None, None, bn_prev, None, 0, True)
                     dA8 = None
-                if _DEFER_WGRAD:
+                if _DEFER_WGRAD and not isinstance(dA_w, GramBN):
                     # issued after the BN-backward pass: the side-stream weight gradient then runs
                     # beside the next (compute-bound) dgrad instead of the memory-bound BN pass
                     _wgrad(conv, dA_w, h_in)
@@ -261,6 +292,8 @@ class BlockFn(torch.autograd.Function):
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
                     fz = BNBwdFuse(pa, pbn, y=pym, x2=pad_, bn2=pds[1] if pds is not None else None)
+                if g_read is not None:
+                    torch.cuda.current_stream().wait_event(g_read)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
                             accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
                 if _DEFER_WGRAD:  # issued by the previous block's backward after its BN pass

@@ -54,9 +54,10 @@ def bn_scale_shift(x: torch.Tensor, bn) -> torch.Tensor:
 
 
 def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
-                  save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False, q8=None, ym=None):
+                  save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False, q8=None, ym=None, colsum=None):
     """``q8 = (y8 uint8, exp int32[1], amax f32[1])``: also write the e4m3 copy of y.
-    ``ym`` (uint8, numel / 8; modes 1 / 2 with ReLU): also write the mask y > 0 as bits."""
+    ``ym`` (uint8, numel / 8; modes 1 / 2 with ReLU): also write the mask y > 0 as bits.
+    ``colsum`` (fp32 [C], zeroed; mode 0): also accumulate the column sums of the stored y."""
     C = x.shape[-1]
     R = x.numel() // C
     y8, e8, a8 = q8 if q8 is not None else (None, None, None)
@@ -64,7 +65,7 @@ def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma
         x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _lib.ptr(x2),
         _lib.ptr(stats2), _lib.ptr(gamma2), _lib.ptr(beta2), y.data_ptr(), _lib.ptr(save),
         _lib.ptr(save2), R, C, mode, 1 if relu else 0, eps, 1 if eval_mode else 0,
-        _lib.ptr(y8), _lib.ptr(e8), _lib.ptr(a8), _lib.ptr(ym), _lib.stream_ptr()), "bn fwd")
+        _lib.ptr(y8), _lib.ptr(e8), _lib.ptr(a8), _lib.ptr(ym), _lib.ptr(colsum), _lib.stream_ptr()), "bn fwd")
 
 
 def relu_mask_bits(y: torch.Tensor) -> torch.Tensor:
@@ -76,7 +77,7 @@ def relu_mask_bits(y: torch.Tensor) -> torch.Tensor:
 
 
 def bn_act_forward(x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2, mode: int, relu: bool,
-                   q8=None, ym: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   q8=None, ym: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Training-mode forward (no autograd): statistics from ``bn.work.slab``;
     ``q8`` / ``ym`` as in :func:`bn_fwd_launch`."""
     y = torch.empty_like(x)
@@ -89,7 +90,8 @@ def bn_act_forward(x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2, mode: i
                   stats2=w2.stats if w2 is not None else None,
                   gamma2=bn2.weight if bn2 is not None else None,
                   beta2=bn2.bias if bn2 is not None else None,
-                  save2=w2.save if w2 is not None else None, mode=mode, relu=relu, eps=bn.eps, q8=q8, ym=ym)
+                  save2=w2.save if w2 is not None else None, mode=mode, relu=relu, eps=bn.eps, q8=q8, ym=ym,
+                  colsum=colsum)
     return y
 
 

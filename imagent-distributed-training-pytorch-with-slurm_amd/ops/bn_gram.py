@@ -1,0 +1,117 @@
+"""A bottleneck's last BatchNorm backward without its apply pass (``csrc/kernels/bn_gram.hip``).
+
+For x3 = conv3(h2) (1x1, p -> 4p) and its BatchNorm bn3 (torchvision Bottleneck, the reference's
+``models.resnet50``, imagenet.py:312; backward :128) the backward output dx3 = A g + B x3 + c is the
+widest activation gradient of the block. Instead of writing it:
+
+* :func:`gram_coef` turns bn3's reductions (accumulated by the producing dgrad's epilogue) into the
+  per-channel (A, B, c) and accumulates dgamma / dbeta;
+* :func:`gram_dgrad` runs conv3's dgrad as ONE GEMM over the concatenated operand [g | h2] with the
+  weights [diag(A) W3 | W3^T diag(B) W3] and the bias c W3, into bn2's fused backward epilogue;
+* :func:`gram_wgrad` forms conv3's weight gradient from g^T h2, the Gram matrix h2^T h2 and the
+  column sums of h2 (side stream), then one fix-up kernel.
+
+h2 (conv3's input, relu(bn2(x2))) has to exist: blocks that take this path keep it materialised
+in forward (``ops/block.py``)."""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib, streams
+from .conv import BNBwdFuse, _base_args, _igemm_call, colsum_into, igemm_wgrad
+from .grad_sink import notify_ready
+
+
+class GramBN:
+    """bn3's backward output dx3 = A g + B x3 + c, kept as (g, coef = [3][4p] (A, B, c))."""
+
+    __slots__ = ("g", "coef")
+
+    def __init__(self, g: torch.Tensor, coef: torch.Tensor):
+        self.g, self.coef = g, coef
+
+
+def gram_coef(bn, g: torch.Tensor) -> GramBN:
+    """(A, B, c) of bn3 from its reduction slab; dgamma / dbeta accumulate as the apply pass would."""
+    w = bn.work
+    C = bn.weight.shape[0]
+    R = g.numel() // C
+    coef = torch.empty((3, C), device=g.device, dtype=torch.float32)
+    _lib.check(_lib.kernels().imk_bn_bwd_coef(w.scratch.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
+                                              bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(), coef.data_ptr(),
+                                              R, C, _lib.stream_ptr()), "bn bwd coef")
+    notify_ready(bn.weight)
+    notify_ready(bn.bias)
+    return GramBN(g, coef)
+
+
+def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tensor:
+    """dh2 = dx3 W3 without dx3: one v3 GEMM over K = [g (4p) | h2 (p)] with bn2's fused
+    backward epilogue (``bnb``; the bias c W3 enters before its ReLU mask)."""
+    N, H, W, C4 = gb.g.shape
+    p = h2.shape[-1]
+    wt = conv.wt_bf16  # [p][1][1][4p] = W3^T
+    assert tuple(wt.shape) == (p, 1, 1, C4) and conv.kh == 1 and conv.stride == 1
+    Wf = wt.view(p, C4).float()
+    Q = torch.mm(Wf * gb.coef[1], Wf.t())  # W3^T diag(B) W3 [p][p] (symmetric)
+    wcat = torch.empty((p, C4 + p), device=h2.device, dtype=torch.bfloat16)
+    bias = torch.empty((p,), device=h2.device, dtype=torch.float32)
+    k = _lib.kernels()
+    st = _lib.stream_ptr()
+    _lib.check(k.imk_bn_gram_dgrad_weights(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), wcat.data_ptr(),
+                                           bias.data_ptr(), p, C4, st), "gram dgrad weights")
+    out = torch.empty((N, H, W, p), device=h2.device, dtype=torch.bfloat16)
+    a = _base_args(gb.g.data_ptr(), wcat.data_ptr(), out.data_ptr(), N, H, W, C4, H, W, p, C4 + p, 1)
+    a.nth, a.ntw, a.dh0, a.dhs, a.dw0, a.dws = 1, 1, 0, 1, 0, 1
+    a.kh0, a.khs, a.kw0, a.kws, a.KW = 0, 1, 0, 1, 1
+    a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, 1, 0, 0, p
+    a.flags = 0
+    a.X2, a.C2 = h2.data_ptr(), p
+    a.bias = bias.data_ptr()
+    bnb.fill(a)
+    _igemm_call(a, 0, st, "conv dgrad (bn3 gram)")
+    return out
+
+
+def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None):
+    """conv3.weight.grad += A (g^T h2) + B (W3 h2^T h2) + c colsum(h2), on the wgrad side stream.
+    ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``).
+    Returns the side-stream event after the last read of ``g`` (or None without a side stream):
+    the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
+    side = streams.side_stream(h2.device) if h2.is_cuda else None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(h2.device))
+    ctx = torch.cuda.stream(side) if side is not None else _Null()
+    with ctx:
+        C4, p = gb.g.shape[-1], h2.shape[-1]
+        T = torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
+        G = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
+        own_s = s is None
+        if own_s:
+            s = torch.zeros((p,), device=h2.device, dtype=torch.float32)
+        igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1)
+        ev = None
+        if side is not None:
+            ev = torch.cuda.Event()
+            ev.record(side)
+        igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
+        if own_s:
+            colsum_into(h2.view(-1, p), s)
+        P = torch.mm(conv.w_bf16.view(C4, p).float(), G)  # W3 G [4p][p]
+        _lib.check(_lib.kernels().imk_bn_gram_wgrad_fixup(conv.weight.grad.data_ptr(), T.data_ptr(), P.data_ptr(),
+                                                          gb.coef.data_ptr(), s.data_ptr(), C4, p,
+                                                          _lib.stream_ptr()), "gram wgrad fixup")
+        notify_ready(conv.weight)
+    if side is not None:
+        streams.protect(gb.g, gb.coef, h2, s)
+        streams.ensure_join_after_backward()
+    return ev
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--epi", type=int, default=0, help="0 auto, 1 direct, 2 LDS-staged epilogue")
     ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3, block-scaled MFMA) forward")
     ap.add_argument("--tiles", default=None, help="comma list of explicit tile ids to time for fwd/dgrad")
+    ap.add_argument("--bnb", action="store_true",
+                    help="also time the dgrad with the fused BatchNorm-backward epilogue (ReLU mask bits, "
+                         "the model's block-output form), for the auto tile and every --tiles id")
     a = ap.parse_args()
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
     dev = "cuda"
@@ -130,6 +133,23 @@ def main():
             line += f" | fp8 fwd {t8:8.1f} {flops / t8 / 1e6:6.0f}"
             r["fp8_fwd_us"] = t8
             tot["fp8_fwd"] += t8 * cnt
+        bnb = None
+        if a.bnb and not stem and Ci % 8 == 0 and k >= s:
+            from imagent_amd.models.resnet import BatchNorm2d, BNWork
+            from imagent_amd.ops import _lib
+            from imagent_amd.ops.bn import relu_mask_bits
+            from imagent_amd.ops.conv import BNBwdFuse
+            bn = BatchNorm2d(Ci).to(dev)
+            xb = torch.randn(B, H, H, Ci, device=dev).to(torch.bfloat16)
+            save = torch.stack([xb.float().reshape(-1, Ci).mean(0), torch.ones(Ci, device=dev)])
+            bn.work = BNWork(torch.zeros(_lib.STAT_SLOTS, 2, Ci, device=dev), torch.zeros(2, Ci, device=dev), save,
+                             torch.zeros(_lib.kernels().imk_bn_bwd_scratch_floats(Ci), device=dev))
+            bits = relu_mask_bits(torch.relu(torch.randn_like(xb)))
+            bnb = BNBwdFuse(xb, bn, y=bits)
+            t_b = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, bnb=bnb))
+            line += f" | dgrad+bnb {t_b:8.1f} ({flops / t_b / 1e6:5.0f} TF)"
+            r["dgrad_bnb_us"] = t_b
+            tot["dgrad_bnb"] += t_b * cnt
         if a.tiles and not stem:
             yref = igemm_fwd(x, w, s, p, k, k).float()
             dref = igemm_dgrad(dy, wt, (H, H), s, p, k, k).float()
@@ -147,6 +167,12 @@ def main():
                     continue
                 line += f"\n      tile {t}: fwd {tf:8.1f} us {flops / tf / 1e6:6.0f} TF | dgrad {td:8.1f} us " \
                         f"{flops / td / 1e6:6.0f} TF | rel err vs auto fwd {ef:.1e} dgrad {ed:.1e}"
+                if bnb is not None:
+                    try:
+                        tb = timeit(lambda: igemm_dgrad(dy, wt, (H, H), s, p, k, k, bnb=bnb, tile=t))
+                        line += f" | dgrad+bnb {tb:8.1f}"
+                    except RuntimeError:
+                        line += " | dgrad+bnb n/a"
                 r[f"tile{t}"] = (tf, td, ef, ed)
                 if ef > 2e-2 or ed > 2e-2:
                     line += "  <-- MISMATCH"

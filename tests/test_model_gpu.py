@@ -93,6 +93,7 @@ def test_bn_operand_fusion_matches_torch(monkeypatch):
     fp32 PyTorch model, as the unfused path is checked (test_hip_vs_torch_forward_backward)."""
     from imagent_amd.ops import block
     monkeypatch.setattr(block, "_XFUSE", True)
+    monkeypatch.setattr(block, "_GRAM", False)  # Gram bn3 blocks keep conv3's input (no operand fusion there)
     calls = []
     real = block.bn_scale_shift
     monkeypatch.setattr(block, "bn_scale_shift", lambda a, bn: calls.append(1) or real(a, bn))
@@ -419,6 +420,22 @@ def test_fused_stem_pool_backward_matches_unfused():
     assert rel(g1, g0) < 5e-3
     assert rel(w1, w0) < 1e-3
     assert rel(b1, b0) < 1e-3
+
+
+def test_bn_gram_backward_matches_torch(monkeypatch):
+    """IMAGENT_BN_GRAM: every identity bottleneck whose backward is premasked (11 of ResNet-50's 16 blocks:
+    not the 4 downsample blocks, not the last one) takes bn3's backward without the apply pass -- conv3's
+    dgrad over [g | h2] with folded weights and bias, its wgrad from g^T h2, the Gram matrix h2^T h2 and
+    colsum(h2) (ops/bn_gram.py). Logits, every parameter gradient and the BN buffers against the fp32
+    PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward)."""
+    from imagent_amd.ops import block
+    monkeypatch.setattr(block, "_GRAM", True)
+    calls = []
+    real_d, real_w = block.gram_dgrad, block.gram_wgrad
+    monkeypatch.setattr(block, "gram_dgrad", lambda *a, **k: calls.append("d") or real_d(*a, **k))
+    monkeypatch.setattr(block, "gram_wgrad", lambda *a, **k: calls.append("w") or real_w(*a, **k))
+    test_hip_vs_torch_forward_backward("resnet50", True)
+    assert calls.count("d") == 11 and calls.count("w") == 11, calls
 
 
 @pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
