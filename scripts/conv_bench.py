@@ -133,6 +133,14 @@ def main():
             line += f" | fp8 fwd {t8:8.1f} {flops / t8 / 1e6:6.0f}"
             r["fp8_fwd_us"] = t8
             tot["fp8_fwd"] += t8 * cnt
+            if Co % 16 == 0:  # dgrad: e5m2 gradient x e4m3 transposed weights
+                g8 = dy.float().to(torch.float8_e5m2).view(torch.uint8)
+                wt8 = wt.float().to(torch.float8_e4m3fn).view(torch.uint8)
+                f8d = (g8, e8[0:1], wt8, e8[1:2])
+                t8d = timeit(lambda: igemm_dgrad(dy, wt8, (H, H), s, p, k, k, fp8=f8d))
+                line += f" | fp8 dgrad {t8d:8.1f} {flops / t8d / 1e6:6.0f}"
+                r["fp8_dgrad_us"] = t8d
+                tot["fp8_dgrad"] += t8d * cnt
         bnb = None
         if a.bnb and not stem and Ci % 8 == 0 and k >= s:
             from imagent_amd.models.resnet import BatchNorm2d, BNWork
@@ -150,6 +158,11 @@ def main():
             line += f" | dgrad+bnb {t_b:8.1f} ({flops / t_b / 1e6:5.0f} TF)"
             r["dgrad_bnb_us"] = t_b
             tot["dgrad_bnb"] += t_b * cnt
+            if a.fp8 and "fp8_dgrad_us" in r:
+                t8b = timeit(lambda: igemm_dgrad(dy, wt8, (H, H), s, p, k, k, bnb=bnb, fp8=f8d))
+                line += f" | fp8 dgrad+bnb {t8b:8.1f}"
+                r["fp8_dgrad_bnb_us"] = t8b
+                tot["fp8_dgrad_bnb"] += t8b * cnt
         if a.tiles and not stem:
             yref = igemm_fwd(x, w, s, p, k, k).float()
             dref = igemm_dgrad(dy, wt, (H, H), s, p, k, k).float()

@@ -26,12 +26,23 @@ def run(args, timeout, extra_env=None):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     t0 = time.time()
-    r = subprocess.run([sys.executable, "-u", "-m", "imagent_amd.cli"] + args, cwd=ROOT, env=env,
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout[-4000:])
-        raise SystemExit(f"training run failed ({r.returncode}): {' '.join(args)}")
-    return r.stdout, time.time() - t0
+    # the child's log is echoed as it arrives (a long run shows progress) and kept for parsing
+    p = subprocess.Popen([sys.executable, "-u", "-m", "imagent_amd.cli"] + args, cwd=ROOT, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    lines = []
+    for line in p.stdout:
+        lines.append(line)
+        sys.stdout.write("    " + line)
+        sys.stdout.flush()
+        if time.time() - t0 > timeout:
+            p.kill()
+            break
+    rc = p.wait()
+    out = "".join(lines)
+    if rc != 0:
+        sys.stderr.write(out[-4000:])
+        raise SystemExit(f"training run failed ({rc}): {' '.join(args)}")
+    return out, time.time() - t0
 
 
 def curve(out):

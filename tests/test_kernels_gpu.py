@@ -500,13 +500,16 @@ def test_fp8_quant_matches_torch_e4m3():
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2])
-@pytest.mark.parametrize("tile", [0, 2, 4, 8])
+@pytest.mark.parametrize("tile", [0, 2, 4, 8, 17, 18, 19])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 2, 0), (3, 16, 11, 64, 3, 1, 1),
                                    (2, 128, 14, 256, 1, 1, 0), (4, 64, 16, 64, 3, 1, 1), (2, 512, 4, 512, 3, 1, 1)])
 def test_conv_fp8_forward(tile, shape, epi):
-    """Block-scaled fp8 MFMA conv vs fp32 conv of the same dequantised operands."""
+    """Block-scaled fp8 MFMA conv vs fp32 conv of the same dequantised operands (tiles 17 / 18 / 19: the
+    v3 main loop with 1-byte operands, C % 128 == 0 and the staged epilogue only; tile 0 takes it there)."""
     from imagent_amd.ops.conv import igemm_fwd
     N, Ci, H, Co, k, s, p = shape
+    if tile >= 17 and (Ci % 128 or epi == 1):
+        pytest.skip("v3 fp8: C % 128 == 0, staged epilogue")
     torch.manual_seed(9)
     ex, ew = -3, -8
     x = torch.randn(N, H, H, Ci, device=DEV).abs() * 4  # post-ReLU-like
