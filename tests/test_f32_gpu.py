@@ -245,6 +245,49 @@ def test_resnet50_f32_forward_backward_matches_float64():
     assert not bad, bad
 
 
+@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_f32_block_node_matches_per_op(arch, split):
+    """BlockF32Fn (one autograd node per residual block: conv1's dgrad accumulates the residual gradient in
+    its epilogue, weight gradients on the side stream) against the per-op autograd nodes on the same weights
+    and input: loss, every gradient and the BatchNorm buffers. Deterministic mode, so both paths take the
+    fixed-order statistics passes and the comparison is exact up to fp32 add order (1e-5)."""
+    import copy
+    from imagent_amd.data.loader import InputTransform
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native_f32 import bind_native_f32
+    from imagent_amd.ops.conv import set_deterministic
+    from imagent_amd.ops.f32 import XentF32Fn, set_split
+    torch.manual_seed(9)
+    base = getattr(resnet, arch)(num_classes=100)
+    u8 = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8, device=DEV)
+    y = torch.randint(0, 100, (4,), device=DEV)
+    xh = InputTransform("hip_f32", (64, 64), cpad=4)(u8)
+    out = []
+    set_deterministic(True)
+    set_split(split)
+    try:
+        for fused in (True, False):
+            m = copy.deepcopy(base)
+            st = bind_native_f32(m, DEV)
+            st.fused_blocks = fused
+            m.train()
+            st.arena.zero_grad()
+            loss = XentF32Fn.apply(m(xh), y, torch.zeros(4, device=DEV), 0.0)
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((loss.item(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                        {n: b.clone() for n, b in m.named_buffers()}))
+    finally:
+        set_split(False)
+        set_deterministic(False)
+    (l1, g1, b1), (l2, g2, b2) = out
+    assert abs(l1 - l2) < 1e-6 * max(1.0, abs(l2)), (l1, l2)
+    bad = [(n, rel(g1[n], g2[n])) for n in g1 if rel(g1[n], g2[n]) > 1e-5]
+    assert not bad, bad
+    assert all(rel(b1[n].float(), b2[n].float()) < 1e-6 for n in b1)
+
+
 def _r18_f32_steps(gfloor, resync):
     import copy
     from imagent_amd.data.loader import InputTransform

@@ -129,12 +129,14 @@ def test_conv_lds_epilogue(tile, shape):
     assert rel(acc.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
-@pytest.mark.parametrize("tile", [17, 18])
+@pytest.mark.parametrize("tile", [17, 18, 30, 31, 32, 33])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 1, 0), (2, 64, 8, 256, 1, 1, 0),
                                    (3, 128, 15, 320, 3, 1, 1), (3, 128, 15, 320, 3, 2, 1), (8, 256, 14, 256, 3, 1, 1),
                                    (2, 128, 9, 192, 1, 1, 0), (3, 64, 5, 192, 3, 2, 1), (2, 512, 7, 2048, 1, 1, 0)])
 def test_conv_v3(tile, shape):
-    """v3 main loop (conv_igemm_v3.h; 17: 256x256, 18: 128x128): buffer-descriptor LDS-DMA whose
+    """v3 main loop (conv_igemm_v3.h; 17: 256x256, 18: 128x128) and the v4 A/B loop (conv_igemm_v4.h, 32x32x16
+    MFMA, one 4-wave block per CU; 30 / 31: 256x256 4- / 3-deep, 32: 256x128, 33: 128x256, profiles/
+    r50_b1024_v4_mfma32_study.md): buffer-descriptor LDS-DMA whose
     out-of-image taps / rows beyond M or Nout read the buffer unit's zeros -- padding borders,
     strided dgrad parity classes (taps with negative offsets), ragged M and N -- forward +
     statistics, dgrad, dgrad accumulate against fp32; 1 to 36 K-tiles."""
@@ -230,6 +232,30 @@ def test_wgrad_halo(N, Ci, Co, H, W):
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, variant
     dw0 = torch.ones(Co, 3, 3, Ci, device=DEV)  # accumulates (+=) into the gradient
     igemm_wgrad(nhwc(g), nhwc(x), dw0, 1, 1, 3, 3, variant=9)
+    assert rel(dw0.permute(0, 3, 1, 2) - 1.0, w.grad) < 5e-3
+
+
+@pytest.mark.parametrize("N,Ci,Co,H,W", [(3, 128, 128, 56, 56), (2, 64, 192, 8, 56), (1, 64, 64, 4, 56),
+                                         (2, 256, 256, 28, 28), (3, 128, 64, 4, 28), (3, 512, 512, 14, 14),
+                                         (1, 64, 128, 14, 14)])
+def test_wgrad_halo_stride2(N, Ci, Co, H, W):
+    """Stride-2 halo-tiled 3x3 weight gradient (conv_wgrad_halo.h, S = 2: the input patch staged as four
+    row / column parity planes) against the fp32 conv weight gradient: output widths 28 / 14 / 7, top / left
+    padding taps, bands crossing images, zero-padded k rows; +=. (Opt-in: IMAGENT_WGRAD_HALO=3; measured slower
+    than the register-staged kernel on the R50 shapes.)"""
+    from imagent_amd.ops.conv import igemm_wgrad
+    torch.manual_seed(12)
+    x = bf(torch.randn(N, Ci, H, W, device=DEV))
+    w = torch.randn(Co, Ci, 3, 3, device=DEV).requires_grad_(True)
+    yr = F.conv2d(x.float(), w, None, 2, 1)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    for variant in (9, 0, -1):  # 0: the default dispatch (register-staged unless IMAGENT_WGRAD_HALO=3)
+        dw = torch.zeros(Co, 3, 3, Ci, device=DEV)
+        igemm_wgrad(nhwc(g), nhwc(x), dw, 2, 1, 3, 3, variant=variant)
+        assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, variant
+    dw0 = torch.ones(Co, 3, 3, Ci, device=DEV)
+    igemm_wgrad(nhwc(g), nhwc(x), dw0, 2, 1, 3, 3, variant=9)
     assert rel(dw0.permute(0, 3, 1, 2) - 1.0, w.grad) < 5e-3
 
 
