@@ -189,6 +189,8 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+        // (the fused BN-backward dgrads on 128x128 tiles with their epilogue operands prefetched instead: within
+        // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken)
         if (a.Nout >= 512 && t8 >= 192 && K >= v3_big_min_k()) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles

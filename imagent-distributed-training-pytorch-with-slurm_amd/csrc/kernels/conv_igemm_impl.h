@@ -420,9 +420,43 @@ __device__ __forceinline__ void epilogue(const IGemmArgs& a, const f32x4 (&acc)[
 // rounding of the new term versus the direct epilogue.)
 // The fragment pass (1) is the caller's functor put(smem, P) (it writes this thread's accumulators as
 // bf16 at [pixel row][channel] with row pitch P bytes), so any MFMA shape can feed it.
+// IG_BNBWD on a dense output grid: the BatchNorm input x (and the mask bits) of this thread's epilogue chunks,
+// loaded into registers at kernel START (epi_prefetch), so their HBM latency hides under the main loop instead
+// of stalling the epilogue after it (v3; the short-K dgrads are epilogue-bound: 1024@14 -> 256 dgrad 251 us,
+// with the fused BN backward 443 us before this)
+template <int BM, int BN, int NT>
+struct EpiPF {
+    static constexpr int CPR = BN / 8, RG = NT / CPR, NQ = BM / RG;
+    u32x4 xo[NQ];
+    uint32_t yo[NQ];
+    bool on;
+};
+
+__device__ __forceinline__ bool epi_dense(const IGemmArgs& a) {
+    return a.YH == a.OH && a.YW == a.OW && a.sY == 1 && a.oy == 0 && a.ox == 0 && !(a.flags & IG_ACCUM_SUB2);
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epi_prefetch(const IGemmArgs& a, EpiPF<BM, BN, NT>& pf, int m0, int n0, int tid) {
+    using PF = EpiPF<BM, BN, NT>;
+    pf.on = (a.flags & IG_BNBWD) && epi_dense(a);
+    if (!pf.on) return;
+    const int cc = tid % PF::CPR, rg = tid / PF::CPR;
+    const int n = n0 + cc * 8;
+    const bool nok = n < a.Nout;
+#pragma unroll
+    for (int q = 0; q < PF::NQ; ++q) {
+        const int m = m0 + rg + PF::RG * q;
+        const bool ok = nok && m < a.M;
+        const long e = (long)(ok ? m : 0) * a.ldy + (nok ? n : 0);
+        pf.xo[q] = ok ? *reinterpret_cast<const u32x4*>(a.bnx + e) : u32x4{0u, 0u, 0u, 0u};
+        pf.yo[q] = (ok && a.bnym) ? a.bnym[e >> 3] : 0u;
+    }
+}
+
 template <int BM, int BN, int NT, class Put>
 __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, char* smem, int m0, int n0, int tid,
-                                                 float* st) {
+                                                 float* st, const EpiPF<BM, BN, NT>* pf = nullptr) {
     constexpr int P = BN * 2 + 16;  // LDS row pitch, bytes
     constexpr int CPR = BN / 8;     // 16-B chunks per row
     constexpr int RG = NT / CPR;    // rows processed concurrently (row groups)
@@ -510,6 +544,10 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
 #pragma unroll
     for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
     const int ohw = a.OH * a.OW;
+    // dense output (every stride-1 conv and dgrad: the output grid IS the row grid): element offset m * ldy + n,
+    // without the two runtime divisions per row chunk of the general (strided-dgrad phase / padded) map
+    const bool dense = epi_dense(a);
+    const bool pfon = pf && pf->on;  // x / mask bits already in registers (epi_prefetch)
     constexpr int QB = 4;  // chunks whose global reads are issued together
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += QB) {
@@ -522,17 +560,27 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
             const int m = m0 + row;
             e[u] = -1;
             if (q0 + u < NQ && m < a.M && nok) {
-                const int img = m / ohw, rem = m - img * ohw;
-                const int oh = rem / a.OW, ow = rem - oh * a.OW;
-                e[u] = (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy + n;
+                bool ov = true;
+                if (dense) {
+                    e[u] = (long)m * a.ldy + n;
+                } else {
+                    const int img = m / ohw, rem = m - img * ohw;
+                    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                    e[u] = (((long)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy + n;
+                    ov = old_valid(a, oh, ow);
+                }
                 if (accum) {
-                    oo[u] = old_valid(a, oh, ow)
-                                ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u])
-                                : u32x4{0u, 0u, 0u, 0u};
+                    oo[u] = ov ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u])
+                               : u32x4{0u, 0u, 0u, 0u};
                 }
                 if (bnb) {
-                    xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
-                    if (has_y) yo[u] = a.bnym[e[u] >> 3];
+                    if (pfon) {
+                        xo[u] = pf->xo[q0 + u];
+                        yo[u] = pf->yo[q0 + u];
+                    } else {
+                        xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                        if (has_y) yo[u] = a.bnym[e[u] >> 3];
+                    }
                     if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
                 }
             }
@@ -632,7 +680,8 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
 // 16x16x32 fragments (lane: 4 channels of one pixel, 8 B) -> the staged epilogue
 template <int BM, int BN, int NT, int FN, int FM>
 __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&acc)[FN][FM], char* smem, int m0,
-                                             int n0, int wrow0, int wcol0, int lane, int tid, float* st) {
+                                             int n0, int wrow0, int wcol0, int lane, int tid, float* st,
+                                             const EpiPF<BM, BN, NT>* pf = nullptr) {
     auto put = [&](char* sm, int P) {
 #pragma unroll
         for (int j = 0; j < FM; ++j)
@@ -643,7 +692,7 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
                 *reinterpret_cast<u32x2*>(sm + row * P + col * 2) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
             }
     };
-    epilogue_lds_put<BM, BN, NT>(a, put, smem, m0, n0, tid, st);
+    epilogue_lds_put<BM, BN, NT>(a, put, smem, m0, n0, tid, st, pf);
 }
 
 // LDS row swizzle of the stage ring: the 16-B chunk a lane's fragment read or DMA

@@ -43,7 +43,17 @@ __device__ __forceinline__ void v3_dma(__amdgpu_buffer_rsrc_t r, char* lds, uint
 }
 
 // RB: LDS row bytes per stage (128: BK 64; 64: BK 32). NS: ring depth.
-template <int BM, int BN, int WN, int NS, int NW, int RB>
+// EB: operand element bytes. 2: bf16 (v_mfma_f32_16x16x32_bf16, two k-steps per 128-B stage); 1: fp8
+// (IG_FP8, conv_igemm_fp8.hip): the same rows hold 128 k, ONE block-scaled v_mfma_scale_f32_16x16x128_f8f6f4
+// per fragment pair and stage -- twice the bf16 MFMA cycles for four times the k, so the same LDS bytes and
+// MFMA time per stage over half the stages. Each lane feeds 32 consecutive k of its row (logical chunks
+// 2g, 2g + 1, g = lane >> 4) for BOTH operands; the per-tensor power-of-two scales ride in the
+// instruction's E8M0 operands. FB: format of the gathered operand (0 e4m3, 1 e5m2 = dgrad's gradient).
+// EB 4: fp32 operands (the fp32 training path's 3 x bf16 split, f32.hip): 128-B rows of 32 fp32 k, each lane
+// reads its 8 k (32 B, chunks 2g, 2g + 1 as fp8) and splits them into bf16 hi + lo in registers; x w =
+// hi hi + hi lo + lo hi on three v_mfma_f32_16x16x32_bf16 (fp32 accumulate, ~2^-16 relative per product);
+// direct fp32 epilogue (+ bias, + accumulate).
+template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -51,8 +61,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     constexpr int RPP = 1024 / RB, CPR = RB / 16;
     constexpr int QA = BM / (RPP * NW), QB = BN / (RPP * NW);
     static_assert(QA >= 1 && QB >= 1 && WM * WN == NW && FN % 2 == 0, "tile / wave split");
+    static_assert(EB == 2 || RB == 128, "fp8 / fp32: 128-B rows (one MFMA k-step per stage)");
     constexpr int LPS = QA + QB;
-    constexpr int KS = RB / 2;        // k (bf16) per stage
+    constexpr int KS = RB / EB;       // k per stage
     constexpr int NKS = RB / 64;      // MFMA k-steps (32) per stage
     constexpr int SAB = BM * RB, SBB = BN * RB;
     constexpr int FH = FN / 2;        // channel fragments per half group
@@ -74,8 +85,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     const int ohw = a.OH * a.OW;
     const int lrow = lane / CPR;
     const int lchunk = (lane % CPR) ^ lds_swz<RB>(lrow);
-    const __amdgpu_buffer_rsrc_t rx = v3_rsrc(a.X, (uint32_t)((size_t)a.N * a.H * a.W * a.C * 2));
-    const __amdgpu_buffer_rsrc_t rw = v3_rsrc(a.Wk, (uint32_t)((size_t)a.Nout * a.ldb * 2));
+    const __amdgpu_buffer_rsrc_t rx = v3_rsrc(a.X, (uint32_t)((size_t)a.N * a.H * a.W * a.C * EB));
+    const __amdgpu_buffer_rsrc_t rw = v3_rsrc(a.Wk, (uint32_t)((size_t)a.Nout * a.ldb * EB));
     const __amdgpu_buffer_rsrc_t rx2 =
         v3_rsrc(a.X2 ? a.X2 : a.X, a.X2 ? (uint32_t)((size_t)a.M * a.C2 * 2) : 0u);
 
@@ -91,7 +102,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
         const int img = mm / ohw, rem = mm - img * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         const int ih0 = oh * a.sA + a.dh0, iw0 = ow * a.sA + a.dw0;
-        xbase[q] = (((int64_t)img * a.H + ih0) * a.W + iw0) * a.C * 2 + lchunk * 16;
+        xbase[q] = (((int64_t)img * a.H + ih0) * a.W + iw0) * a.C * EB + lchunk * 16;
         uint32_t mk = 0;
         for (int ti = 0; ti < a.nth; ++ti) {
             const int ih = ih0 + ti * a.dhs;
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
         const int n = n0 + (wid * QB + q) * RPP + lrow;
-        vw[q] = n < a.Nout ? (uint32_t)(n * a.ldb * 2 + lchunk * 16) : OOB_OFF;
+        vw[q] = n < a.Nout ? (uint32_t)(n * a.ldb * EB + lchunk * 16) : OOB_OFF;
     }
 
     // issue cursor: tap (ti, tj) = t, channel stage cs within the tap
@@ -121,8 +132,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     int xtap = 0, wtap = 0;  // uniform: byte offset of the tap in X, weight column of the tap
     auto set_tap = [&]() {
         const int dh = iti * a.dhs, dw = itj * a.dws;
-        xtap = (dh * a.W + dw) * a.C * 2;
-        wtap = ((a.kh0 + iti * a.khs) * a.KW + (a.kw0 + itj * a.kws)) * a.C * 2;
+        xtap = (dh * a.W + dw) * a.C * EB;
+        wtap = ((a.kh0 + iti * a.khs) * a.KW + (a.kw0 + itj * a.kws)) * a.C * EB;
 #pragma unroll
         for (int q = 0; q < QA; ++q)
             vx[q] = (xmask[q] >> it) & 1 ? (uint32_t)(xbase[q] + xtap) : OOB_OFF;
@@ -160,6 +171,11 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     set_tap();
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p) issue_next();
+    // the fused BN backward's x / mask-bit chunks (128x128 bf16 tiles: the short-K dgrads): issued after the
+    // prologue stages, landing under the main loop (the first stage wait covers them)
+    constexpr bool PFE = EB == 2 && BM == 128 && BN == 128 && NW == 4;
+    EpiPF<BM, BN, NW * 64> pf;
+    if constexpr (PFE) epi_prefetch<BM, BN, NW * 64>(a, pf, m0, n0, tid);
 
     f32x4 acc[FN][FM];
 #pragma unroll
@@ -174,6 +190,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     int fk[2];
     fk[0] = (((lane >> 4) + 0) ^ lds_swz<RB>(fr)) * 8;
     fk[1] = (((lane >> 4) + 4) ^ lds_swz<RB>(fr)) * 8;
+    // fp8: the lane's 32 bytes are logical chunks 2g, 2g + 1 of its row (byte offsets); E8M0 scales
+    const int f8c0 = ((2 * (lane >> 4)) ^ lds_swz<RB>(fr)) * 16, f8c1 = ((2 * (lane >> 4) + 1) ^ lds_swz<RB>(fr)) * 16;
+    const int sx8 = EB == 1 ? 127 + a.xexp[0] : 127, sw8 = EB == 1 ? 127 + a.wexp[0] : 127;
     for (int s = 0; s < nk; ++s) {
         if (is - 1 - s >= NS - 2)
             __builtin_amdgcn_s_waitcnt((((NS - 2) * LPS) & 0xF) | ((((NS - 2) * LPS) >> 4) << 14) | (0x7 << 4) |
@@ -183,6 +202,69 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
         __builtin_amdgcn_s_barrier();
         issue_next();
         const int buf = s % NS;
+        if constexpr (EB == 1) {
+            // one 128-deep k-step: pixel fragments + channel half 0 first, half 1 read under half 0's MFMAs
+            const char* cx = sX + buf * SAB + (wm * TM + fr) * RB;
+            const char* cw = sW + buf * SBB + (wn * TN + fr) * RB;
+            auto rd8 = [&](const char* p) {
+                const u32x4 lo = *reinterpret_cast<const u32x4*>(p + f8c0);
+                const u32x4 hi = *reinterpret_cast<const u32x4*>(p + f8c1);
+                return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            };
+            i32x8 gx[FM], gw[FN];
+#pragma unroll
+            for (int j = 0; j < FM; ++j) gx[j] = rd8(cx + j * 16 * RB);
+#pragma unroll
+            for (int i = 0; i < FH; ++i) gw[i] = rd8(cw + i * 16 * RB);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * (FM + FH), 0);
+#pragma unroll
+            for (int i = FH; i < FN; ++i) gw[i] = rd8(cw + i * 16 * RB);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * FH, 0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(gw[i], gx[j], acc[i][j], 0, FB, 0, sw8,
+                                                                                  0, sx8);
+            __builtin_amdgcn_sched_group_barrier(0x8, FN * FM, 0);
+            __builtin_amdgcn_s_setprio(0);
+            continue;
+        }
+        if constexpr (EB == 4) {
+            // one 32-deep k-step: 8 fp32 k per lane -> bf16 hi / lo fragments
+            const char* cx = sX + buf * SAB + (wm * TM + fr) * RB;
+            const char* cw = sW + buf * SBB + (wn * TN + fr) * RB;
+            auto rds = [&](const char* p, bf16x8& hi, bf16x8& lo) {
+                const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + f8c0);
+                const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + f8c1);
+                const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                u32x4 h, l;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    h[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+                    l[k] = pack_bf2(v[2 * k] - lo_bf(h[k]), v[2 * k + 1] - hi_bf(h[k]));
+                }
+                hi = __builtin_bit_cast(bf16x8, h);
+                lo = __builtin_bit_cast(bf16x8, l);
+            };
+            bf16x8 xh[FM], xl[FM], wh[FN], wl[FN];
+#pragma unroll
+            for (int j = 0; j < FM; ++j) rds(cx + j * 16 * RB, xh[j], xl[j]);
+#pragma unroll
+            for (int i = 0; i < FN; ++i) rds(cw + i * 16 * RB, wh[i], wl[i]);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FM; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[i], xh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], xl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], xh[j], acc[i][j], 0, 0, 0);
+                }
+            __builtin_amdgcn_s_setprio(0);
+            continue;
+        }
         const bf16_t* bx = reinterpret_cast<const bf16_t*>(sX + buf * SAB + (wm * TM + fr) * RB);
         const bf16_t* bw = reinterpret_cast<const bf16_t*>(sW + buf * SBB + (wn * TN + fr) * RB);
         // groups g = (ks, h): h = 0 reads the k-step's pixel fragments + channel half 0, h = 1
@@ -224,15 +306,45 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
         }
         __builtin_amdgcn_s_setprio(0);
     }
+    if constexpr (EB == 4) {  // fp32 out: lane holds channels nb + i*16 + 4g + r of pixel mb + j*16 + fr
+        const int g = lane >> 4;
+        const bool accum = a.flags & IG_ACCUM;
+        if (!accum) {  // (+ bias) (+ the BatchNorm statistics as shifted sums into the slab, DPP-reduced)
+            epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + 4 * g, m0 + wm * TM + fr, lane, st);
+            return;
+        }
+        float* Y = reinterpret_cast<float*>(a.Y);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+            const int m = m0 + wm * TM + j * 16 + fr;
+            if (m >= a.M) continue;
+            const int img = m / ohw, rem = m - img * ohw;
+            const int oh = rem / a.OW, ow = rem - oh * a.OW;
+            float* yp = Y + (((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int n = n0 + wn * TN + i * 16 + 4 * g;
+                if (n >= a.Nout) continue;  // Nout % 4 == 0 (host)
+                f32x4 v = acc[i][j];
+                if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + n);
+                f32x4* p = reinterpret_cast<f32x4*>(yp + n);
+                if (accum) v += *p;
+                *p = v;
+            }
+        }
+        return;
+    }
     __syncthreads();  // every DMA retired (last wait) and every wave done reading: the ring is free
-    epilogue_lds<BM, BN, NW * 64, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st);
+    epilogue_lds<BM, BN, NW * 64, FN, FM>(a, acc, smem, m0, n0, wm * TM, wn * TN, lane, tid, st,
+                                          PFE ? &pf : nullptr);
 }
 
-template <int BM, int BN, int WN, int NS, int NW, int RB>
+template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0>
 int launch_v3(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-    const size_t lds = std::max((size_t)NS * (BM + BN) * RB, epi_lds_bytes(BM, BN, NW * 64));
-    hipLaunchKernelGGL((igemm_v3_kernel<BM, BN, WN, NS, NW, RB>), dim3(ntiles), dim3(NW * 64), lds, st, a);
+    const size_t lds = EB == 4 ? (size_t)NS * (BM + BN) * RB
+                               : std::max((size_t)NS * (BM + BN) * RB, epi_lds_bytes(BM, BN, NW * 64));
+    hipLaunchKernelGGL((igemm_v3_kernel<BM, BN, WN, NS, NW, RB, EB, FB>), dim3(ntiles), dim3(NW * 64), lds, st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
@@ -252,6 +364,26 @@ inline bool v3_ok(const IGemmArgs& a) {
                  a.ldb < a.C + a.C2 || (size_t)a.M * a.C2 * 2 >= (1ull << 31)))
         return false;
     const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
+    return xb < (1ull << 31) && wb < (1ull << 31);
+}
+
+// fp32 (3 x bf16 split, EB = 4) shapes v3 covers: C % 32 == 0 (one tap per 32-deep stage), fp32 out with
+// optional bias / accumulate, Nout and ldy % 4 == 0 (16-B stores)
+inline bool v3_ok32(const IGemmArgs& a) {
+    if (a.C % 32 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
+    if ((a.flags & ~(IG_ACCUM | IG_OUT_F32)) || !(a.flags & IG_OUT_F32)) return false;
+    if ((a.stats && (a.flags & IG_ACCUM)) || a.xbn || a.X2 || a.Nout % 4 || a.ldy % 4) return false;
+    const size_t xb = (size_t)a.N * a.H * a.W * a.C * 4, wb = (size_t)a.Nout * a.ldb * 4;
+    return xb < (1ull << 31) && wb < (1ull << 31);
+}
+
+// fp8 shapes v3 covers (EB = 1): C % 128 == 0 (one tap per 128-deep stage), the staged bf16 epilogue
+// (statistics, fused BN backward, accumulate), no second K segment, scales present
+inline bool v3_ok8(const IGemmArgs& a) {
+    if (!(a.flags & IG_FP8) || a.C % 128 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
+    if (a.flags & (IG_OUT_F32 | IG_STEM | IG_RELU | IG_AFFINE | IG_EPI_DIRECT)) return false;
+    if (a.bias || a.xbn || a.X2 || !a.xexp || !a.wexp || a.Nout % 8 || a.ldy % 8) return false;
+    const size_t xb = (size_t)a.N * a.H * a.W * a.C, wb = (size_t)a.Nout * a.ldb;
     return xb < (1ull << 31) && wb < (1ull << 31);
 }
 

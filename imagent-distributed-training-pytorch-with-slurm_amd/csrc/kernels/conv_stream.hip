@@ -467,6 +467,17 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
         if (bn == 128) return launch_stream<128, 128, 2>(a, st);
         return launch_stream<128, 64, 2>(a, st);
     }
+    // K = 256 BN-backward dgrads into wide outputs (bottleneck conv1 dgrads 256 -> 512 @28, 256 -> 1024 @14): 64-channel
+    // weight slices resident in LDS (as the K = 256 forwards) instead of the one-tile-per-block v3 loop, whose
+    // 4-stage main loop leaves these epilogue-heavy GEMMs latency-bound. IMAGENT_STREAM_BNB256=0: v3 (A/B)
+    static const bool bnb256 = [] {
+        const char* e = getenv("IMAGENT_STREAM_BNB256");
+        return !e || atoi(e) != 0;
+    }();
+    if (a.C == 256 && (a.flags & IG_BNBWD) && a.Nout > 128 && bnb256) {
+        if (a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 3>(a, st) : 1;
+        return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
+    }
     // K = 256 into <= 128 channels (bottleneck conv1 256 -> 64 / 128): 64-channel
     // slices, plain epilogue
     if (a.C == 256 && a.Nout <= 128) {

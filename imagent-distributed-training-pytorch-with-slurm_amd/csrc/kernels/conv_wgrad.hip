@@ -332,13 +332,14 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
             default: return launch_wgrad_v3<64, 2>(a, splits, st);
         }
     }
-    // 3x3 stride 1 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
-    // 1 only 64 -> 64, 2 (default) every shape it covers
+    // 3x3 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
+    // 1 only 64 -> 64, 2 (default) every stride-1 shape it covers, 3 also the stride-2 phase-plane form (measured
+    // slower than the register-staged kernel on every R50 stride-2 shape, profiles/r50_b1024_round4_kernel_ab.md)
     static const int halo = [] {
         const char* e = getenv("IMAGENT_WGRAD_HALO");
         return e ? atoi(e) : 2;
     }();
-    if (halo && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
+    if (halo && (a.stride == 1 || halo >= 3) && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
     // 2 % slower than this register-staged loop on every R50 shape: not kept)

@@ -20,6 +20,7 @@
 //    argmax, global average pool, FC bias column sums, input normalisation to fp32.
 
 #include "conv_igemm_impl.h"
+#include "conv_igemm_v3.h"
 
 namespace {
 
@@ -969,21 +970,49 @@ IMK_EXPORT int imk_set_f32_split(int on) {
     return 0;
 }
 
+// a.stats (a [STAT_SLOTS][2][Nout] slab, zeroed; shifted by a.shift): the BatchNorm statistics of the output,
+// accumulated by the v3 split kernel's epilogue -> returns 0; any other kernel leaves the slab alone and returns
+// 2 (the caller runs the statistics pass)
 IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
     const IGemmArgs& a = *args;
     if (a.M <= 0 || a.Nout <= 0) return 0;
     if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32))) return -100;
     const int ntiles = ((a.M + F_BM - 1) / F_BM) * ((a.Nout + F_BN - 1) / F_BN);
     const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);  // (= the split kernel's 2 x 4 bf16 planes)
+    // split arithmetic, C % 32 == 0: the v3 LDS-DMA ring with fp32 rows (conv_igemm_v3.h, EB = 4; IMAGENT_F32_V3=0:
+    // the register-staged kernel below, A/B)
+    static const bool v3 = [] {
+        const char* e = getenv("IMAGENT_F32_V3");
+        return !e || atoi(e) != 0;
+    }();
+    if (g_f32_split && v3 && v3_ok32(a)) {
+        const int r = a.Nout <= 64 ? launch_v3<128, 64, 1, 2, 4, 128, 4>(a, (hipStream_t)stream)
+                                   : launch_v3<128, 128, 2, 2, 4, 128, 4>(a, (hipStream_t)stream);
+        return r;
+    }
+    IGemmArgs b = a;
+    b.stats = nullptr;  // the kernels below have no statistics epilogue
+    const int nost = a.stats ? 2 : 0;
     if (g_f32_split) {
         if (a.C % F_BK == 0)
-            hipLaunchKernelGGL(igemm_f32s_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+            hipLaunchKernelGGL(igemm_f32s_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, b);
         else
-            hipLaunchKernelGGL(igemm_f32s_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+            hipLaunchKernelGGL(igemm_f32s_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, b);
     } else if (a.C % F_BK == 0)
-        hipLaunchKernelGGL(igemm_f32_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(igemm_f32_kernel<0>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, b);
     else
-        hipLaunchKernelGGL(igemm_f32_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(igemm_f32_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, b);
+    IMK_CHECK_LAUNCH();
+    return nost;
+}
+
+// training statistics from a conv epilogue's [STAT_SLOTS][2][C] slab of sums shifted by `shift` (imk_conv_f32
+// with a.stats): save <- (mean, rstd), running stats updated (as imk_bn_stats_f32, one launch, no pass over x)
+IMK_EXPORT int imk_bn_fold_slab_f32(const float* slab, const float* shift, float* save, float* rmean, float* rvar,
+                                    long R, int C, float eps, float momentum, void* stream) {
+    if (C <= 0 || R <= 0) return -100;
+    hipLaunchKernelGGL(bn_fold_fwd_f32_kernel, dim3((C + FOLD_CH - 1) / FOLD_CH), dim3(256), 0, (hipStream_t)stream,
+                       slab, STAT_SLOTS, shift, save, rmean, rvar, R, C, eps, momentum);
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -151,6 +151,7 @@ def _declare(name: str, lib) -> None:
             "imk_wgrad_f32": [vp, vp, vp] + [i32] * 11 + [vp],
             "imk_bn_slab_floats_f32": [i32],
             "imk_bn_stats_f32": [vp, vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],
+            "imk_bn_fold_slab_f32": [vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],
             "imk_bn_apply_f32": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
             "imk_bn_bwd_f32": [vp] * 11 + [i64, i32, vp],
             "imk_maxpool_f32": [vp, vp, vp] + [i32] * 9 + [vp],

@@ -16,7 +16,7 @@ from typing import Optional, Sequence, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, streams
 from .conv import _base_args, conv_out_size
 from .grad_sink import notify_ready
 
@@ -35,8 +35,12 @@ def set_split(on: bool) -> None:
 
 def conv_f32(x: torch.Tensor, wk: torch.Tensor, stride: int, pad: int, KH: int, KW: int,
              bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-             accumulate: bool = False) -> torch.Tensor:
-    """y[N,OH,OW,Co] (+)= conv(x[N,H,W,Ci], wk[Co][KH][KW][Ci]) (+ bias), fp32 NHWC."""
+             accumulate: bool = False, stats: Optional[torch.Tensor] = None,
+             shift: Optional[torch.Tensor] = None):
+    """y[N,OH,OW,Co] (+)= conv(x[N,H,W,Ci], wk[Co][KH][KW][Ci]) (+ bias), fp32 NHWC.
+    ``stats`` ([STAT_SLOTS, 2, Co] fp32, zeroed; ``shift`` [Co]): also accumulate the output's BatchNorm
+    statistics as sums shifted by ``shift`` in the conv epilogue (the v3 split kernel); then returns
+    (y, fused) -- fused False when the kernel taking this shape has no statistics epilogue."""
     N, H, W, Ci = x.shape
     Co = wk.shape[0]
     assert x.dtype == torch.float32 and wk.dtype == torch.float32 and x.is_contiguous() and wk.is_contiguous()
@@ -50,21 +54,30 @@ def conv_f32(x: torch.Tensor, wk: torch.Tensor, stride: int, pad: int, KH: int, 
     a.flags = 1 | (8 if accumulate else 0)
     if bias is not None:
         a.bias = bias.data_ptr()
-    _lib.check(_k().imk_conv_f32(C.byref(a), _lib.stream_ptr()), "conv f32")
+    if stats is not None:
+        a.stats = stats.data_ptr()
+        a.shift = _lib.ptr(shift)
+    rc = _k().imk_conv_f32(C.byref(a), _lib.stream_ptr())
+    if rc != 2:
+        _lib.check(rc, "conv f32")
+    if stats is not None:
+        return out, rc == 0
     return out
 
 
 def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int, KH: int,
-              KW: int) -> torch.Tensor:
-    """dx[N,H,W,Ci] = dgrad(dy[N,OH,OW,Co], wt[Ci][KH][KW][Co]); strided convs as one launch per output
+              KW: int, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci][KH][KW][Co]); strided convs as one launch per output
     parity class touching only the taps that reach it (the bf16 path's sub-pixel decomposition,
-    ops/conv.py igemm_dgrad)."""
+    ops/conv.py igemm_dgrad). ``accumulate``: added to ``out`` in the epilogue (the residual gradient)."""
     N, OH, OW, Co = dy.shape
     Ci = wt.shape[0]
     H, W = in_hw
-    out = torch.empty((N, H, W, Ci), device=dy.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty((N, H, W, Ci), device=dy.device, dtype=torch.float32)
+        accumulate = False
     S = stride
-    if S > 1 and (KH < S or KW < S):
+    if S > 1 and (KH < S or KW < S) and not accumulate:
         out.zero_()  # parity classes no tap reaches stay 0
     for ph in range(S):
         for pw in range(S):
@@ -81,7 +94,7 @@ def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride
             a.dw0, a.dws = (pw + pad - kw0) // S, -1
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
-            a.flags = 1
+            a.flags = 1 | (8 if accumulate else 0)
             _lib.check(_k().imk_conv_f32(C.byref(a), _lib.stream_ptr()), "conv dgrad f32")
     return out
 
@@ -107,14 +120,34 @@ def _weight_nhwc(mod, cpad: int = 0) -> torch.Tensor:
     return w.contiguous()
 
 
+def _stats_slab(bn) -> torch.Tensor:
+    """The per-BatchNorm [STAT_SLOTS, 2, C] slab the producing conv's epilogue fills (zeroed here)."""
+    s = getattr(bn, "_f32_slab", None)
+    if s is None or s.device != bn.weight.device:
+        s = torch.zeros((_lib.STAT_SLOTS, 2, bn.num_features), device=bn.weight.device, dtype=torch.float32)
+        bn._f32_slab = s
+    else:
+        s.zero_()
+    return s
+
+
 class ConvF32Fn(torch.autograd.Function):
     """NHWC fp32 conv; the weight gradient lands in the parameter's arena slot (``weight.grad``) and
-    the bucketed reducer is notified, as ``ops.conv.ConvFn`` does on the bf16 path."""
+    the bucketed reducer is notified, as ``ops.conv.ConvFn`` does on the bf16 path. The dgrad (critical
+    path) is issued first; the weight gradient runs on the side stream (``ops/streams.py``) beside the
+    next layers' backward when the overlap is on."""
 
     @staticmethod
-    def forward(ctx, x, weight, mod):
+    def forward(ctx, x, weight, mod, bn=None):
+        """``bn``: the training BatchNorm that consumes y -- its batch statistics come out of this conv's
+        epilogue when the kernel has one (``bn._f32_stats_ready``; :func:`bn_train_f32` folds them)."""
         wk = _weight_nhwc(mod, x.shape[-1])
-        y = conv_f32(x, wk, mod.stride, mod.padding, mod.kh, mod.kw)
+        if bn is not None:
+            y, fused = conv_f32(x, wk, mod.stride, mod.padding, mod.kh, mod.kw, stats=_stats_slab(bn),
+                                shift=bn.running_mean)
+            bn._f32_stats_ready = fused
+        else:
+            y = conv_f32(x, wk, mod.stride, mod.padding, mod.kh, mod.kw)
         ctx.mod = mod
         ctx.save_for_backward(x, wk)
         return y
@@ -129,15 +162,30 @@ class ConvF32Fn(torch.autograd.Function):
             wt = wk.permute(3, 1, 2, 0).contiguous()  # [Ci][KH][KW][Co]
             dx = dgrad_f32(dy, wt, (x.shape[1], x.shape[2]), mod.stride, mod.padding, mod.kh, mod.kw)
         g = mod.weight.grad.permute(0, 2, 3, 1)  # arena view, [Co][KH][KW][Ci] memory
-        if x.shape[-1] != mod.in_channels:  # stem: 4-channel input, 3-channel weight
-            gp = torch.zeros_like(wk)
-            wgrad_f32(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw)
-            g.add_(gp[..., : mod.in_channels])
-        else:
-            assert g.is_contiguous()
-            wgrad_f32(dy, x, g, mod.stride, mod.padding, mod.kh, mod.kw)
-        notify_ready(mod.weight)
-        return dx, None, None
+        side = streams.side_stream(dy.device) if dy.is_cuda else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(dy.device))
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            if x.shape[-1] != mod.in_channels:  # stem: 4-channel input, 3-channel weight
+                gp = torch.zeros_like(wk)
+                wgrad_f32(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw)
+                g.add_(gp[..., : mod.in_channels])
+            else:
+                assert g.is_contiguous()
+                wgrad_f32(dy, x, g, mod.stride, mod.padding, mod.kh, mod.kw)
+            notify_ready(mod.weight)
+        if side is not None:
+            streams.protect(dy, x)
+            streams.ensure_join_after_backward()
+        return dx, None, None, None
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class LinearF32Fn(torch.autograd.Function):
@@ -184,10 +232,16 @@ def bn_train_f32(x: torch.Tensor, bn, ws: F32Workspace, res: Optional[torch.Tens
     C = x.shape[-1]
     R = x.numel() // C
     save = torch.empty(2, C, device=x.device, dtype=torch.float32)
-    # the running mean is the shift of the (shifted) sums: close to the batch mean
-    _lib.check(_k().imk_bn_stats_f32(x.data_ptr(), bn.running_mean.data_ptr(), ws.slab.data_ptr(),
-                                     save.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(), R, C,
-                                     float(bn.eps), float(bn.momentum), _lib.stream_ptr()), "bn stats f32")
+    if getattr(bn, "_f32_stats_ready", False):  # the producing conv's epilogue summed them (ConvF32Fn bn=)
+        bn._f32_stats_ready = False
+        _lib.check(_k().imk_bn_fold_slab_f32(bn._f32_slab.data_ptr(), bn.running_mean.data_ptr(), save.data_ptr(),
+                                             bn.running_mean.data_ptr(), bn.running_var.data_ptr(), R, C,
+                                             float(bn.eps), float(bn.momentum), _lib.stream_ptr()), "bn fold f32")
+    else:
+        # the running mean is the shift of the (shifted) sums: close to the batch mean
+        _lib.check(_k().imk_bn_stats_f32(x.data_ptr(), bn.running_mean.data_ptr(), ws.slab.data_ptr(),
+                                         save.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(), R,
+                                         C, float(bn.eps), float(bn.momentum), _lib.stream_ptr()), "bn stats f32")
     bn.num_batches_tracked.add_(1)
     y = torch.empty_like(x)
     _lib.check(_k().imk_bn_apply_f32(x.data_ptr(), save.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
@@ -233,6 +287,121 @@ class BNF32Fn(torch.autograd.Function):
         notify_ready(bn.weight)
         notify_ready(bn.bias)
         return dx, dres, None, None, None
+
+
+# ------------------------------------------------------------------ residual block
+def _bn_bwd(g, y, x, save, bn, ws, want_dres: bool):
+    """BN(+ReLU from ``y``) backward of ``g``: (dx, g' = masked g | None); dgamma / dbeta into the arena."""
+    C = x.shape[-1]
+    R = x.numel() // C
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if want_dres else None
+    _lib.check(_k().imk_bn_bwd_f32(g.data_ptr(), _lib.ptr(y), x.data_ptr(), save.data_ptr(), bn.weight.data_ptr(),
+                                   ws.slab.data_ptr(), ws.red.data_ptr(), bn.weight.grad.data_ptr(),
+                                   bn.bias.grad.data_ptr(), dx.data_ptr(), _lib.ptr(dres), R, C, _lib.stream_ptr()),
+               "bn bwd f32")
+    notify_ready(bn.weight)
+    notify_ready(bn.bias)
+    return dx, dres
+
+
+def _conv_bn_stats(x, conv, bn, fuse: bool):
+    """conv_f32 whose epilogue also sums ``bn``'s training statistics when ``fuse`` (bn_train_f32 folds them)."""
+    wk = _weight_nhwc(conv, x.shape[-1])
+    if not fuse:
+        return conv_f32(x, wk, conv.stride, conv.padding, conv.kh, conv.kw)
+    y, fused = conv_f32(x, wk, conv.stride, conv.padding, conv.kh, conv.kw, stats=_stats_slab(bn),
+                        shift=bn.running_mean)
+    bn._f32_stats_ready = fused
+    return y
+
+
+def _wgrad_side(mod, dy, x) -> None:
+    """The weight gradient into the arena on the side stream (beside the rest of the backward)."""
+    side = streams.side_stream(dy.device) if dy.is_cuda else None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(dy.device))
+    with torch.cuda.stream(side) if side is not None else _nullctx():
+        g = mod.weight.grad.permute(0, 2, 3, 1)
+        assert g.is_contiguous()
+        wgrad_f32(dy, x, g, mod.stride, mod.padding, mod.kh, mod.kw)
+        notify_ready(mod.weight)
+    if side is not None:
+        streams.protect(dy, x)
+        streams.ensure_join_after_backward()
+
+
+def _dgrad(mod, dy, x_shape, out=None, accumulate=False):
+    wt = _weight_nhwc(mod).permute(3, 1, 2, 0).contiguous()  # [Ci][KH][KW][Co]
+    return dgrad_f32(dy, wt, (x_shape[1], x_shape[2]), mod.stride, mod.padding, mod.kh, mod.kw, out=out,
+                     accumulate=accumulate)
+
+
+class BlockF32Fn(torch.autograd.Function):
+    """One torchvision residual block (BasicBlock / Bottleneck, with or without downsample) on the fp32
+    kernels as ONE autograd node, as the bf16 path's ``ops.block`` does: forward convs with the BatchNorm
+    statistics in their epilogues (not in deterministic mode), BN(+residual)(+ReLU) passes; backward
+    hand-scheduled: the block-input gradient starts as the residual branch's masked gradient (or the
+    downsample dgrad) and conv1's dgrad ACCUMULATES into it in its epilogue (no separate add), every
+    weight gradient on the side stream (reference: the torchvision blocks of ``imagenet.py:312``,
+    backward ``:128``)."""
+
+    @staticmethod
+    def forward(ctx, x, block, ws):
+        from .conv import deterministic
+        fuse = not deterministic()
+        pairs = block.convs_bns()
+        h = x
+        saved, saves = [x], []
+        for conv, bn, _ in pairs[:-1]:
+            a = _conv_bn_stats(h, conv, bn, fuse)
+            h, sv = bn_train_f32(a, bn, ws, None, True)
+            saved += [a, h]
+            saves.append(sv)
+        conv, bn, _ = pairs[-1]
+        a = _conv_bn_stats(h, conv, bn, fuse)
+        ds = block.downsample
+        ad = svd = None
+        idt = x
+        if ds is not None:
+            ad = _conv_bn_stats(x, ds[0], ds[1], fuse)
+            idt, svd = bn_train_f32(ad, ds[1], ws, None, False)
+        y, sv = bn_train_f32(a, bn, ws, idt, True)
+        saves.append(sv)
+        ctx.block, ctx.ws, ctx.n = block, ws, len(pairs)
+        ctx.save_for_backward(*saved, a, ad, y, svd, *saves)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        t = ctx.saved_tensors
+        n, block, ws = ctx.n, ctx.block, ctx.ws
+        x = t[0]
+        acts = [t[1 + 2 * i] for i in range(n - 1)]
+        hs = [t[2 + 2 * i] for i in range(n - 1)]
+        a_last, ad, y, svd = t[2 * n - 1], t[2 * n], t[2 * n + 1], t[2 * n + 2]
+        saves = t[2 * n + 3:]
+        pairs = block.convs_bns()
+        ds = block.downsample
+        g = g.contiguous()
+        dA, dres = _bn_bwd(g, y, a_last, saves[-1], pairs[-1][1], ws, True)
+        if ds is not None:
+            dAd, _ = _bn_bwd(dres, None, ad, svd, ds[1], ws, False)
+            dX = _dgrad(ds[0], dAd, x.shape)
+            _wgrad_side(ds[0], dAd, x)
+        else:
+            dX = dres  # the identity branch's gradient; conv1's dgrad accumulates into it
+        inputs = [x] + hs
+        for i in range(n - 1, -1, -1):
+            conv = pairs[i][0]
+            if i > 0:
+                dH = _dgrad(conv, dA, inputs[i].shape)
+                _wgrad_side(conv, dA, inputs[i])
+                dA, _ = _bn_bwd(dH, hs[i - 1], acts[i - 1], saves[i - 1], pairs[i - 1][1], ws, False)
+            else:
+                _dgrad(conv, dA, x.shape, out=dX, accumulate=True)
+                _wgrad_side(conv, dA, x)
+        return dX, None, None
 
 
 # ------------------------------------------------------------------ pooling, loss, input
