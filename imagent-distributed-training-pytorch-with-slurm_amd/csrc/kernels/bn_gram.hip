@@ -88,7 +88,43 @@ __global__ __launch_bounds__(256) void bn_gram_wgrad_fixup_kernel(float* __restr
     }
 }
 
+// As bn_bwd_coef_kernel, with sum(g xhat) NOT from the slab but from T = g^T h2 (the weight gradient's GEMM):
+// x3 = h2 W3^T, so sum_m g[m][o] x3[m][o] = sum_i W3[o][i] T[o][i] and sum(g xhat) = rstd (that - mean sum(g)).
+// The producing dgrad then never reads x3 (BNBwdFuse without x). One wave per channel.
+__global__ __launch_bounds__(256) void bn_bwd_coef_T_kernel(const float* __restrict__ slab, const float* __restrict__ T,
+                                                            const bf16_t* __restrict__ w, const float* __restrict__ save,
+                                                            const float* __restrict__ gamma, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta, float* __restrict__ coef, int S,
+                                                            int C, int p, float inv_cnt) {
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (o >= C) return;  // wave-uniform
+    float dot = 0.f, sg = 0.f;
+    for (int i = lane; i < p; i += 64) dot += bf2f(w[(size_t)o * p + i]) * T[(size_t)o * p + i];
+    for (int s = lane; s < S; s += 64) sg += slab[(size_t)s * 3 * C + C + o];
+    dot = wave_sum(dot);
+    sg = wave_sum(sg);
+    if (lane) return;
+    const float mean = save[o], rstd = save[C + o], gr = gamma[o] * rstd;
+    const float sgx = rstd * (dot - mean * sg);
+    if (dgamma) dgamma[o] += sgx;
+    if (dbeta) dbeta[o] += sg;
+    const float k0 = -gr * inv_cnt * sg, kx = -gr * inv_cnt * sgx * rstd;
+    coef[o] = gr;
+    coef[C + o] = kx;
+    coef[2 * C + o] = k0 - kx * mean;
+}
+
 }  // namespace
+
+IMK_EXPORT int imk_bn_bwd_coef_T(const float* scratch, const float* T, const void* w, const float* save,
+                                 const float* gamma, float* dgamma_acc, float* dbeta_acc, float* coef, long R, int C,
+                                 int p, void* stream) {
+    if (R <= 0 || C <= 0 || p <= 0) return -100;
+    hipLaunchKernelGGL(bn_bwd_coef_T_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, scratch, T,
+                       (const bf16_t*)w, save, gamma, dgamma_acc, dbeta_acc, coef, BWD_SLOTS_G, C, p, 1.f / (float)R);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
 
 IMK_EXPORT int imk_bn_bwd_coef(const float* scratch, const float* save, const float* gamma, float* dgamma_acc,
                                float* dbeta_acc, float* coef, long R, int C, void* stream) {

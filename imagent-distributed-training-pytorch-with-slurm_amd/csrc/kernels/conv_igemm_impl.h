@@ -449,7 +449,7 @@ __device__ __forceinline__ void epi_prefetch(const IGemmArgs& a, EpiPF<BM, BN, N
         const int m = m0 + rg + PF::RG * q;
         const bool ok = nok && m < a.M;
         const long e = (long)(ok ? m : 0) * a.ldy + (nok ? n : 0);
-        pf.xo[q] = ok ? *reinterpret_cast<const u32x4*>(a.bnx + e) : u32x4{0u, 0u, 0u, 0u};
+        pf.xo[q] = (ok && a.bnx) ? *reinterpret_cast<const u32x4*>(a.bnx + e) : u32x4{0u, 0u, 0u, 0u};
         pf.yo[q] = (ok && a.bnym) ? a.bnym[e >> 3] : 0u;
     }
 }
@@ -578,7 +578,8 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
                         xo[u] = pf->xo[q0 + u];
                         yo[u] = pf->yo[q0 + u];
                     } else {
-                        xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                        // (bnx null: the bits give the mask, sum(g xhat) is formed elsewhere -- bn_gram.hip)
+                        xo[u] = a.bnx ? *reinterpret_cast<const u32x4*>(a.bnx + e[u]) : u32x4{0u, 0u, 0u, 0u};
                         if (has_y) yo[u] = a.bnym[e[u] >> 3];
                     }
                     if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);

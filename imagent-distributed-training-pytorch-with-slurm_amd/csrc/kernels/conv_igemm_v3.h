@@ -309,6 +309,48 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     if constexpr (EB == 4) {  // fp32 out: lane holds channels nb + i*16 + 4g + r of pixel mb + j*16 + fr
         const int g = lane >> 4;
         const bool accum = a.flags & IG_ACCUM;
+        if (a.flags & IG_BNBWD) {
+            // dgrad into a ReLU'd BatchNorm (fp32, bnx = its input x, bnsave = (mean, rstd)): the stored value is
+            // g' = g * (bn(x) > 0) -- bn(x) computed as the apply kernel computes it -- and the 2-row slab slot
+            // receives sum(g'), sum(g' xhat) (the fp32 backward fold's layout, f32.hip bn_fold_bwd_f32_kernel)
+            const float* X = reinterpret_cast<const float*>(a.bnx);
+            float* Y = reinterpret_cast<float*>(a.Y);
+            float* sb = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) {
+                const int n = n0 + wn * TN + i * 16 + 4 * g;
+                const bool nok = n < a.Nout;  // Nout % 4 == 0 (host)
+                float mu[4], rs[4], sc[4], sh[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    mu[r] = nok ? a.bnsave[n + r] : 0.f;
+                    rs[r] = nok ? a.bnsave[a.Nout + n + r] : 0.f;
+                    sc[r] = nok ? rs[r] * a.bngamma[n + r] : 0.f;
+                    sh[r] = nok ? a.bnbeta[n + r] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < FM; ++j) {
+                    const int m = m0 + wm * TM + j * 16 + fr;
+                    if (m >= a.M || !nok) continue;
+                    const int img = m / ohw, rem = m - img * ohw;
+                    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+                    const size_t e =
+                        (((size_t)img * a.YH + oh * a.sY + a.oy) * a.YW + ow * a.sY + a.ox) * a.ldy + n;
+                    const f32x4 xv = *reinterpret_cast<const f32x4*>(X + e);
+                    f32x4 v = acc[i][j];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float o = (xv[r] - mu[r]) * sc[r] + sh[r];
+                        if (!(o > 0.f)) v[r] = 0.f;
+                        s1[r] += v[r];
+                        s2[r] += v[r] * ((xv[r] - mu[r]) * rs[r]);
+                    }
+                    *reinterpret_cast<f32x4*>(Y + e) = v;
+                }
+                stat_pair_atomic(s1, s2, sb, sb + a.Nout, n, a.Nout, lane);  // every lane (DPP)
+            }
+            return;
+        }
         if (!accum) {  // (+ bias) (+ the BatchNorm statistics as shifted sums into the slab, DPP-reduced)
             epilogue_tile<FN, FM>(a, acc, n0 + wn * TN + 4 * g, m0 + wm * TM + fr, lane, st);
             return;
@@ -371,8 +413,11 @@ inline bool v3_ok(const IGemmArgs& a) {
 // optional bias / accumulate, Nout and ldy % 4 == 0 (16-B stores)
 inline bool v3_ok32(const IGemmArgs& a) {
     if (a.C % 32 || a.nth * a.ntw > 32 || a.nth < 1 || a.ntw < 1) return false;
-    if ((a.flags & ~(IG_ACCUM | IG_OUT_F32)) || !(a.flags & IG_OUT_F32)) return false;
+    if ((a.flags & ~(IG_ACCUM | IG_OUT_F32 | IG_BNBWD)) || !(a.flags & IG_OUT_F32)) return false;
     if ((a.stats && (a.flags & IG_ACCUM)) || a.xbn || a.X2 || a.Nout % 4 || a.ldy % 4) return false;
+    if ((a.flags & IG_BNBWD) && (!a.stats || !a.bnx || !a.bnsave || !a.bngamma || !a.bnbeta || a.bias ||
+                                 (a.flags & IG_ACCUM)))
+        return false;
     const size_t xb = (size_t)a.N * a.H * a.W * a.C * 4, wb = (size_t)a.Nout * a.ldb * 4;
     return xb < (1ull << 31) && wb < (1ull << 31);
 }

@@ -233,7 +233,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                                    : u32x4{0u, 0u, 0u, 0u};
                     }
                     if (bnb) {
-                        xo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
+                        // bnx null (mask bits given): slot 0 of the slab is then not sum(g xhat) (bn_gram.hip forms
+                        // it from g^T h2) and x is never read
+                        xo[u] = a.bnx ? *reinterpret_cast<const u32x4*>(a.bnx + e[u]) : u32x4{0u, 0u, 0u, 0u};
                         if (has_y) yo[u] = a.bnym[e[u] >> 3];
                         if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
                     }

@@ -976,7 +976,7 @@ IMK_EXPORT int imk_set_f32_split(int on) {
 IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
     const IGemmArgs& a = *args;
     if (a.M <= 0 || a.Nout <= 0) return 0;
-    if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32))) return -100;
+    if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32 | IG_BNBWD))) return -100;
     const int ntiles = ((a.M + F_BM - 1) / F_BM) * ((a.Nout + F_BN - 1) / F_BN);
     const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);  // (= the split kernel's 2 x 4 bf16 planes)
     // split arithmetic, C % 32 == 0: the v3 LDS-DMA ring with fp32 rows (conv_igemm_v3.h, EB = 4; IMAGENT_F32_V3=0:
@@ -991,7 +991,8 @@ IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
         return r;
     }
     IGemmArgs b = a;
-    b.stats = nullptr;  // the kernels below have no statistics epilogue
+    b.stats = nullptr;  // the kernels below have no statistics / BN-backward epilogue
+    b.flags &= ~IG_BNBWD;
     const int nost = a.stats ? 2 : 0;
     if (g_f32_split) {
         if (a.C % F_BK == 0)
@@ -1004,6 +1005,27 @@ IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
         hipLaunchKernelGGL(igemm_f32_kernel<1>, dim3(ntiles), dim3(256), lds, (hipStream_t)stream, b);
     IMK_CHECK_LAUNCH();
     return nost;
+}
+
+// BatchNorm backward whose masked gradient g' and reductions came from the producing dgrad's epilogue (imk_conv_f32
+// with IG_BNBWD: slab [STAT_SLOTS][2][C] = sum(g'), sum(g' xhat)): fold (dgamma / dbeta +=) + apply pass
+IMK_EXPORT int imk_bn_bwd_slab_f32(const float* g, const float* x, const float* save, const float* gamma,
+                                   const float* slab, float* red, float* dgamma, float* dbeta, float* dx, long R, int C,
+                                   void* stream) {
+    if (C % 4 || R <= 0) return -100;
+    hipLaunchKernelGGL(bn_fold_bwd_f32_kernel, dim3((C + FOLD_CH - 1) / FOLD_CH), dim3(256), 0, (hipStream_t)stream,
+                       slab, STAT_SLOTS, red, dgamma, dbeta, C);
+    IMK_CHECK_LAUNCH();
+    const long n4 = R * C / 4;
+    const int grid = sgrid(n4);
+    if ((long)grid * 1024 % C == 0)
+        hipLaunchKernelGGL(bn_bwd_apply_f32_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, g, nullptr, x,
+                           save, gamma, red, dx, nullptr, n4, C, 1.f / (float)R);
+    else
+        hipLaunchKernelGGL(bn_bwd_apply_f32_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, g, nullptr,
+                           x, save, gamma, red, dx, nullptr, n4, C, 1.f / (float)R);
+    IMK_CHECK_LAUNCH();
+    return 0;
 }
 
 // training statistics from a conv epilogue's [STAT_SLOTS][2][C] slab of sums shifted by `shift` (imk_conv_f32

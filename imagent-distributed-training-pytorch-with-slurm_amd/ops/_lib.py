@@ -152,6 +152,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_slab_floats_f32": [i32],
             "imk_bn_stats_f32": [vp, vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],
             "imk_bn_fold_slab_f32": [vp, vp, vp, vp, vp, i64, i32, f32, f32, vp],
+            "imk_bn_bwd_slab_f32": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_apply_f32": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
             "imk_bn_bwd_f32": [vp] * 11 + [i64, i32, vp],
             "imk_maxpool_f32": [vp, vp, vp] + [i32] * 9 + [vp],
@@ -182,6 +183,7 @@ def _declare(name: str, lib) -> None:
             "imk_xent_fwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_xent_bwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_colsum_bf16": [vp, vp, i32, i32, vp],
+            "imk_bn_bwd_coef_T": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_gram_dgrad_weights": [vp, i32, vp, vp, vp, vp, i32, i32, vp],
             "imk_bn_gram_wgrad_fixup": [vp, vp, vp, vp, vp, i32, i32, vp],

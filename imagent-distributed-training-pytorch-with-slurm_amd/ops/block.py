@@ -33,7 +33,7 @@ import torch
 from . import streams
 from . import conv as _conv
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_scale_shift
-from .bn_gram import GramBN, gram_coef, gram_dgrad, gram_wgrad
+from .bn_gram import GramBN, gram_T, gram_coef, gram_dgrad, gram_wgrad
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
@@ -62,6 +62,9 @@ _HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
 # (ops/bn_gram.py): conv3's dgrad runs over [g | h2] with folded weights, its wgrad from g^T h2 and the
 # Gram matrix of h2. conv3's input h2 is then kept (no operand-path BN fusion for that conv).
 _GRAM = os.environ.get("IMAGENT_BN_GRAM", "1") != "0"
+# with it, the next block's conv1 dgrad does not read x3 for bn3's sum(g xhat): x3 = h2 W3^T, so that sum is
+# rowsum(W3 * g^T h2) -- the weight gradient's GEMM (IMAGENT_BN_GRAM=slab: from the epilogue's x3 read, A/B)
+_GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
 
 
 def _gram_ok(block, q, x) -> bool:
@@ -199,6 +202,8 @@ class BlockFn(torch.autograd.Function):
         ctx.xbn = xbn
         ctx.gram = gram
         ctx.h2sum = h2sum
+        block._gram = gram  # the next block's conv1 dgrad may then skip reading x3 (BNBwdFuse without x)
+        block._bnb_nox = False
         ctx.save_for_backward(*saved)
         return out
 
@@ -242,7 +247,10 @@ class BlockFn(torch.autograd.Function):
                              fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
         elif premasked and ctx.gram and fuse:
-            dA = gram_coef(bn_l, dout)  # dx3 kept as (g, A, B, c): no apply pass (ops/bn_gram.py)
+            # dx3 kept as (g, A, B, c): no apply pass (ops/bn_gram.py); when the next block's dgrad ran without x3,
+            # sum(g xhat3) comes from T = g^T h2 (formed here, reused by the weight gradient)
+            T = gram_T(dout, outs[-1]) if getattr(block, "_bnb_nox", False) else None
+            dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
             dX = dout
         elif premasked:
             g8a = q.grad_out(a_last, bn_l) if q is not None else None
@@ -254,6 +262,7 @@ class BlockFn(torch.autograd.Function):
         streams.flush_deferred()  # the next block's conv1 wgrad, after this memory-bound BN pass
         block._last_bn = None
         block._bnb_done = False
+        block._bnb_nox = False
         xbn = ctx.xbn  # xbn[i]: conv i's input is BN(acts[i - 1]) + ReLU applied on its operand path
         g_read = None  # side-stream event after the Gram wgrad's last read of dout (= dX)
         for i in range(n - 1, -1, -1):
@@ -287,11 +296,15 @@ class BlockFn(torch.autograd.Function):
             else:
                 prev = getattr(block, "_prev_block", None)
                 fz = None
+                nox = False
                 if fuse and prev is not None and prev._last_bn is not None:
                     pa, pad_, pym = prev._last_bn
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
-                    fz = BNBwdFuse(pa, pbn, y=pym, x2=pad_, bn2=pds[1] if pds is not None else None)
+                    # the previous block's bn3 backward takes the Gram form: sum(g xhat3) from g^T h2, x3 not read
+                    nox = _GRAM_NOX and getattr(prev, "_gram", False) and pds is None and pym is not None
+                    fz = BNBwdFuse(None if nox else pa, pbn, y=pym, x2=pad_,
+                                   bn2=pds[1] if pds is not None else None)
                 if g_read is not None:
                     torch.cuda.current_stream().wait_event(g_read)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
@@ -302,4 +315,5 @@ class BlockFn(torch.autograd.Function):
                     conv_wgrad(conv, dA, h_in)
                 if fz is not None:
                     prev._bnb_done = True
+                    prev._bnb_nox = nox
         return dX, None

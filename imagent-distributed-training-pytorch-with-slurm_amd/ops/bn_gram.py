@@ -24,26 +24,45 @@ from .grad_sink import notify_ready
 
 
 class GramBN:
-    """bn3's backward output dx3 = A g + B x3 + c, kept as (g, coef = [3][4p] (A, B, c))."""
+    """bn3's backward output dx3 = A g + B x3 + c, kept as (g, coef = [3][4p] (A, B, c)); T = g^T h2 when
+    it was formed for the coefficients (``gram_T``)."""
 
-    __slots__ = ("g", "coef")
+    __slots__ = ("g", "coef", "T")
 
-    def __init__(self, g: torch.Tensor, coef: torch.Tensor):
-        self.g, self.coef = g, coef
+    def __init__(self, g: torch.Tensor, coef: torch.Tensor, T: torch.Tensor = None):
+        self.g, self.coef, self.T = g, coef, T
 
 
-def gram_coef(bn, g: torch.Tensor) -> GramBN:
-    """(A, B, c) of bn3 from its reduction slab; dgamma / dbeta accumulate as the apply pass would."""
+def gram_T(g: torch.Tensor, h2: torch.Tensor) -> torch.Tensor:
+    """T = g^T h2 [4p][p] fp32 (conv3's weight-gradient GEMM), on the current stream."""
+    C4, p = g.shape[-1], h2.shape[-1]
+    T = torch.zeros((C4, p), device=g.device, dtype=torch.float32)
+    igemm_wgrad(g, h2, T, 1, 0, 1, 1)
+    return T
+
+
+def gram_coef(bn, g: torch.Tensor, T: torch.Tensor = None, w3: torch.Tensor = None) -> GramBN:
+    """(A, B, c) of bn3 from its reduction slab; dgamma / dbeta accumulate as the apply pass would.
+    ``T`` (= g^T h2) and ``w3`` (conv3's bf16 weight [4p][p]): sum(g xhat) from them instead of the slab
+    (the producing dgrad ran without x, BNBwdFuse(None, ...): one read of x3 less)."""
     w = bn.work
     C = bn.weight.shape[0]
     R = g.numel() // C
     coef = torch.empty((3, C), device=g.device, dtype=torch.float32)
-    _lib.check(_lib.kernels().imk_bn_bwd_coef(w.scratch.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
-                                              bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(), coef.data_ptr(),
-                                              R, C, _lib.stream_ptr()), "bn bwd coef")
+    if T is not None:
+        p = T.shape[1]
+        assert w3.numel() == C * p and w3.dtype == torch.bfloat16
+        _lib.check(_lib.kernels().imk_bn_bwd_coef_T(w.scratch.data_ptr(), T.data_ptr(), w3.data_ptr(),
+                                                    w.save.data_ptr(), bn.weight.data_ptr(),
+                                                    bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
+                                                    coef.data_ptr(), R, C, p, _lib.stream_ptr()), "bn bwd coef T")
+    else:
+        _lib.check(_lib.kernels().imk_bn_bwd_coef(w.scratch.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
+                                                  bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
+                                                  coef.data_ptr(), R, C, _lib.stream_ptr()), "bn bwd coef")
     notify_ready(bn.weight)
     notify_ready(bn.bias)
-    return GramBN(g, coef)
+    return GramBN(g, coef, T)
 
 
 def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tensor:
@@ -85,16 +104,18 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None):
     ctx = torch.cuda.stream(side) if side is not None else _Null()
     with ctx:
         C4, p = gb.g.shape[-1], h2.shape[-1]
-        T = torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
         G = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
         own_s = s is None
         if own_s:
             s = torch.zeros((p,), device=h2.device, dtype=torch.float32)
-        igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1)
         ev = None
-        if side is not None:
-            ev = torch.cuda.Event()
-            ev.record(side)
+        T = gb.T
+        if T is None:  # (else formed on the main stream for the coefficients: g is not read here)
+            T = torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
+            igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1)
+            if side is not None:
+                ev = torch.cuda.Event()
+                ev.record(side)
         igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
         if own_s:
             colsum_into(h2.view(-1, p), s)
@@ -104,7 +125,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None):
                                                           _lib.stream_ptr()), "gram wgrad fixup")
         notify_ready(conv.weight)
     if side is not None:
-        streams.protect(gb.g, gb.coef, h2, s)
+        streams.protect(gb.g, gb.coef, h2, s, T)
         streams.ensure_join_after_backward()
     return ev
 

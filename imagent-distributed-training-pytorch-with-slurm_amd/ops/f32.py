@@ -66,10 +66,13 @@ def conv_f32(x: torch.Tensor, wk: torch.Tensor, stride: int, pad: int, KH: int, 
 
 
 def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride: int, pad: int, KH: int,
-              KW: int, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+              KW: int, out: Optional[torch.Tensor] = None, accumulate: bool = False, bnb=None):
     """dx[N,H,W,Ci] (+)= dgrad(dy[N,OH,OW,Co], wt[Ci][KH][KW][Co]); strided convs as one launch per output
     parity class touching only the taps that reach it (the bf16 path's sub-pixel decomposition,
-    ops/conv.py igemm_dgrad). ``accumulate``: added to ``out`` in the epilogue (the residual gradient)."""
+    ops/conv.py igemm_dgrad). ``accumulate``: added to ``out`` in the epilogue (the residual gradient).
+    ``bnb = (x, save, bn)``: dx is the upstream gradient of that ReLU'd BatchNorm (input x, save = (mean,
+    rstd)): the epilogue stores it masked and sums the BN-backward reductions into ``bn._f32_slab``; returns
+    (dx, fused) -- fused False when the kernel taking the shape has no such epilogue (dx then unmasked)."""
     N, OH, OW, Co = dy.shape
     Ci = wt.shape[0]
     H, W = in_hw
@@ -79,6 +82,8 @@ def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride
     S = stride
     if S > 1 and (KH < S or KW < S) and not accumulate:
         out.zero_()  # parity classes no tap reaches stay 0
+    fused = bnb is not None
+    slab = _stats_slab(bnb[2]) if bnb is not None else None
     for ph in range(S):
         for pw in range(S):
             gh, gw = (H - ph + S - 1) // S, (W - pw + S - 1) // S
@@ -95,7 +100,17 @@ def dgrad_f32(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stride
             a.kh0, a.khs, a.kw0, a.kws, a.KW = kh0, S, kw0, S, KW
             a.YH, a.YW, a.sY, a.oy, a.ox, a.ldy = H, W, S, ph, pw, Ci
             a.flags = 1 | (8 if accumulate else 0)
-            _lib.check(_k().imk_conv_f32(C.byref(a), _lib.stream_ptr()), "conv dgrad f32")
+            if bnb is not None:
+                x, save, bn = bnb
+                a.flags |= 32  # IG_BNBWD
+                a.bnx, a.bnsave, a.stats = x.data_ptr(), save.data_ptr(), slab.data_ptr()
+                a.bngamma, a.bnbeta = bn.weight.data_ptr(), bn.bias.data_ptr()
+            rc = _k().imk_conv_f32(C.byref(a), _lib.stream_ptr())
+            if rc != 2:
+                _lib.check(rc, "conv dgrad f32")
+            fused = fused and rc == 0
+    if bnb is not None:
+        return out, fused
     return out
 
 
@@ -305,6 +320,20 @@ def _bn_bwd(g, y, x, save, bn, ws, want_dres: bool):
     return dx, dres
 
 
+def _bn_bwd_slab(g, x, save, bn, ws):
+    """BN backward of a gradient the producing dgrad already masked and reduced (dgrad_f32 ``bnb``)."""
+    C = x.shape[-1]
+    R = x.numel() // C
+    dx = torch.empty_like(x)
+    _lib.check(_k().imk_bn_bwd_slab_f32(g.data_ptr(), x.data_ptr(), save.data_ptr(), bn.weight.data_ptr(),
+                                        bn._f32_slab.data_ptr(), ws.red.data_ptr(), bn.weight.grad.data_ptr(),
+                                        bn.bias.grad.data_ptr(), dx.data_ptr(), R, C, _lib.stream_ptr()),
+               "bn bwd slab f32")
+    notify_ready(bn.weight)
+    notify_ready(bn.bias)
+    return dx
+
+
 def _conv_bn_stats(x, conv, bn, fuse: bool):
     """conv_f32 whose epilogue also sums ``bn``'s training statistics when ``fuse`` (bn_train_f32 folds them)."""
     wk = _weight_nhwc(conv, x.shape[-1])
@@ -331,10 +360,10 @@ def _wgrad_side(mod, dy, x) -> None:
         streams.ensure_join_after_backward()
 
 
-def _dgrad(mod, dy, x_shape, out=None, accumulate=False):
+def _dgrad(mod, dy, x_shape, out=None, accumulate=False, bnb=None):
     wt = _weight_nhwc(mod).permute(3, 1, 2, 0).contiguous()  # [Ci][KH][KW][Co]
     return dgrad_f32(dy, wt, (x_shape[1], x_shape[2]), mod.stride, mod.padding, mod.kh, mod.kw, out=out,
-                     accumulate=accumulate)
+                     accumulate=accumulate, bnb=bnb)
 
 
 class BlockF32Fn(torch.autograd.Function):
@@ -374,6 +403,8 @@ class BlockF32Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        from .conv import deterministic
+        fuse = not deterministic()  # BN-backward reductions in the inner dgrads' epilogues
         t = ctx.saved_tensors
         n, block, ws = ctx.n, ctx.block, ctx.ws
         x = t[0]
@@ -395,9 +426,17 @@ class BlockF32Fn(torch.autograd.Function):
         for i in range(n - 1, -1, -1):
             conv = pairs[i][0]
             if i > 0:
-                dH = _dgrad(conv, dA, inputs[i].shape)
+                bn_prev = pairs[i - 1][1]
+                fused = False
+                if fuse:
+                    dH, fused = _dgrad(conv, dA, inputs[i].shape, bnb=(acts[i - 1], saves[i - 1], bn_prev))
+                else:
+                    dH = _dgrad(conv, dA, inputs[i].shape)
                 _wgrad_side(conv, dA, inputs[i])
-                dA, _ = _bn_bwd(dH, hs[i - 1], acts[i - 1], saves[i - 1], pairs[i - 1][1], ws, False)
+                if fused:  # dH is already masked; its reductions are in bn_prev's slab
+                    dA = _bn_bwd_slab(dH, acts[i - 1], saves[i - 1], bn_prev, ws)
+                else:
+                    dA, _ = _bn_bwd(dH, hs[i - 1], acts[i - 1], saves[i - 1], bn_prev, ws, False)
             else:
                 _dgrad(conv, dA, x.shape, out=dX, accumulate=True)
                 _wgrad_side(conv, dA, x)
