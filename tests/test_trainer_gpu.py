@@ -54,7 +54,9 @@ def _curve(out):
 WARM = ["--warmup-epochs", "0.5"]
 # the variant / A-B-switch tests only ask "does it learn": at lr 0.05 a run can still leave the basin after
 # it has learned the task (measured: accum2 epoch means 0.65 -> 1.59; IMAGENT_BN_SHIFT=0 1.47 -> 3.79 over
-# 40 iterations, both passing on other runs of the same build), so they train at a calmer lr
+# 40 iterations, both passing on other runs of the same build), so they train at a calmer lr. The fp32
+# PyTorch oracle does the same at lr 0.05 with --accum-steps 2 (last-epoch train loss 1.06 / 0.29 / 1.21 over
+# three seeds, 71.1 % validation top-1 on one; profiles/convergence_r50.md, round-4 table)
 CALM = ["--lr", "0.02"]
 
 
