@@ -107,7 +107,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if ((a.flags & IG_ACCUM) && (a.flags & IG_OUT_F32)) return -103;
     if ((a.flags & IG_BNBWD) && ((a.flags & (IG_OUT_F32 | IG_RELU)) || a.Nout % 8 || a.ldy != a.Nout ||
                                  // no x (bn_gram.hip: sum(g xhat) comes from g^T h2): mask bits, staged epilogue
-                                 (!a.bnx && (!a.bnym || a.bnx2 || (a.flags & IG_EPI_DIRECT))) ||
+                                 (!a.bnx && (!a.bnym || (a.flags & IG_EPI_DIRECT))) ||
                                  !a.bnsave || !a.stats || (!a.bnym && (!a.bngamma || !a.bnbeta)) ||
                                  (a.bnx2 && !a.bnsave2)))
         return -104;

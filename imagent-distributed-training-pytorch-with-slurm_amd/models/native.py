@@ -68,6 +68,19 @@ class NativeState:
             self.fp8 = Fp8State(self)
             for b in blocks:
                 b._q8 = self.fp8
+            self._fp8_outputs()
+
+    def _fp8_outputs(self) -> None:
+        """Which block outputs need an e4m3 copy: those whose next block reads fp8 in its conv1 or downsample
+        conv (``ops.block.fp8_fwd_ok``); the stem pool's likewise for the first block."""
+        from ..ops.block import fp8_fwd_ok
+        blocks = list(self.model.blocks())
+
+        def reads8(b):
+            return fp8_fwd_ok(b.conv1) or (b.downsample is not None and fp8_fwd_ok(b.downsample[0]))
+        for k, b in enumerate(blocks):
+            b._q8_out = k + 1 < len(blocks) and reads8(blocks[k + 1])
+        self._q8_pool = bool(blocks) and reads8(blocks[0])
 
     # ------------------------------------------------------------ shadows
     def _bind_shadows(self):
@@ -127,6 +140,7 @@ class NativeState:
             self.fp8 = Fp8State(self)
             for b in self.model.blocks():
                 b._q8 = self.fp8
+            self._fp8_outputs()
         self.refresh_shadows(full=True)
 
     # ---------------------------------------------------------- workspace
@@ -191,10 +205,11 @@ class NativeState:
 
 
 class Fp8State:
-    """fp8 forward (``--dtype fp8``): e4m3 shadows of the non-stem conv weights
-    (exact per-step scales) and e4m3 copies of every activation a conv reads
-    (delayed per-tensor scales, written by the producing BN / pool). The
-    backward stays bf16 (bf16 weight shadows, bf16 saved activations)."""
+    """fp8 (``--dtype fp8``): e4m3 shadows of the non-stem conv weights (exact per-step scales), e4m3
+    copies of the activations an fp8 forward conv reads and e5m2 copies of the gradients an fp8 dgrad reads
+    (delayed per-tensor scales, written by the producing BN / pool pass). Which convs run fp8 is per shape
+    (``ops.block.fp8_fwd_ok`` / ``fp8_dgrad_ok``: where the 1-byte v3 loop measured faster); weight
+    gradients and everything else stay bf16."""
 
     def __init__(self, st: "NativeState", backward: bool = True):
         from ..ops.fp8 import E5M2_MAX, ActScales, WeightQuantizer
@@ -312,7 +327,7 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
     else:
         y = _bn(y, model.bn1, True, train)
         y = MaxPoolFn.apply(y, 3, 2, 1)
-    if q is not None:
+    if q is not None and getattr(st, "_q8_pool", True):
         q8 = q.out_for(y, q.pool_slot)
         if q8 is not None:
             from ..ops.fp8 import quant_act

@@ -30,7 +30,7 @@ import os
 
 import torch
 
-from . import streams
+from . import _lib, streams
 from . import conv as _conv
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_scale_shift
 from .bn_gram import GramBN, gram_T, gram_coef, gram_dgrad, gram_wgrad
@@ -70,7 +70,7 @@ _GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
 def _gram_ok(block, q, x) -> bool:
     """Does this block's backward take bn3 through the Gram form (forward keeps h2)?"""
     pairs = block.convs_bns()
-    if not (_GRAM and q is None and x.is_cuda and len(pairs) == 3 and block.downsample is None):
+    if not (_GRAM and x.is_cuda and len(pairs) == 3):  # (with fp8: conv3's dgrad stays bf16 in this form)
         return False
     if not getattr(block, "_fuse_bnb", False):  # the next block's dgrad must reduce bn3 (premasked backward)
         return False
@@ -81,7 +81,7 @@ def _gram_ok(block, q, x) -> bool:
 
 def _xfuse_ok(conv, a, q) -> bool:
     """Can ``conv`` (the consumer of BN(a) + ReLU) apply that BN on its operand path?"""
-    if not (_XFUSE and q is None and a.is_cuda) or _conv._NOSTREAM:
+    if not (_XFUSE and (q is None or not fp8_fwd_ok(conv)) and a.is_cuda) or _conv._NOSTREAM:
         return False
     if conv.kh == 1 and conv.kw == 1:
         return (conv.stride == 1 and conv.padding == 0 and conv.in_channels in (64, 128)
@@ -99,9 +99,30 @@ def _fwd(conv, h, bn):
                      stats=bn.work, stem=getattr(conv, "stem", False))
 
 
+# --dtype fp8 runs a conv on the 1-byte v3 loop only where that measured faster than the bf16 kernels
+# (per-shape table: profiles/r50_b1024_fp8_v3_kernel_stats.md); everywhere else, and for everything the bf16
+# path fuses (operand-path BN, the Gram-form bn3 backward), the step stays bf16 and no fp8 copy is written.
+def fp8_fwd_ok(conv) -> bool:
+    """Forward on fp8: 3x3 with >= 128 input channels, 1x1 with >= 512, or 256 into <= 128 channels (the
+    1x1 convs with K <= 256 into wide outputs are HBM streams the bf16 streaming kernel runs faster)."""
+    ci, co = conv.in_channels, conv.out_channels
+    if conv.kh > 1:
+        return ci >= 128
+    return ci >= 512 or (ci == 256 and co <= 128)
+
+
+def fp8_dgrad_ok(conv) -> bool:
+    """dgrad on fp8 (it gathers over the gradient's out_channels): 3x3 with >= 128, 1x1 with >= 512, or 256
+    into <= 128 input channels (256 into wider: the bf16 streaming BN-backward dgrad wins)."""
+    ci, co = conv.in_channels, conv.out_channels
+    if conv.kh > 1:
+        return co >= 128
+    return co >= 512 or (co == 256 and ci <= 128)
+
+
 def _fwd8(conv, h, h8, bn):
-    """fp8 forward (``Fp8State``) when the input has an e4m3 copy, else bf16."""
-    if h8 is None or conv.in_channels % 16:
+    """fp8 forward (``Fp8State``) when the input has an e4m3 copy and the shape is one fp8 wins, else bf16."""
+    if h8 is None or conv.in_channels % 16 or not fp8_fwd_ok(conv):
         return _fwd(conv, h, bn)
     return igemm_fwd(h8[0], conv.w8, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work,
                      fp8=(h8[1], conv.w8_exp))
@@ -114,7 +135,7 @@ def _use8(q, g8):
 
 def _dg8(d8, conv):
     """fp8 dgrad operands (e5m2 gradient, e4m3 transposed weights) or None (bf16)."""
-    if d8 is None or getattr(conv, "wt8", None) is None or conv.out_channels % 16:
+    if d8 is None or getattr(conv, "wt8", None) is None or conv.out_channels % 16 or not fp8_dgrad_ok(conv):
         return None
     return (d8[0], d8[1], conv.wt8, conv.w8_exp)
 
@@ -160,7 +181,7 @@ class BlockFn(torch.autograd.Function):
                 h, h8 = a, None
                 saved += [a, None]
                 continue
-            q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
+            q8 = q.out_for(a, q.slot[id(bn)]) if (q is not None and fp8_fwd_ok(pairs[i + 1][0])) else None
             if gram and i + 1 == len(pairs) - 1:
                 h2sum = torch.zeros(a.shape[-1], device=a.device, dtype=torch.float32)
             h = bn_act_forward(a, None, bn, None, 0, True, q8=q8, colsum=h2sum)
@@ -171,7 +192,8 @@ class BlockFn(torch.autograd.Function):
             a = igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
         else:
             a = _fwd8(conv, h, h8, bn)
-        q8 = q.out_for(a, q.slot[id(bn)]) if q is not None else None
+        # the block output's e4m3 copy only when the next block's conv1 or downsample conv reads fp8
+        q8 = q.out_for(a, q.slot[id(bn)]) if (q is not None and getattr(block, "_q8_out", True)) else None
         # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue (1/16
         # of the bytes of re-reading the output there)
         fuse_next = getattr(block, "_fuse_bnb", False)
@@ -231,9 +253,21 @@ class BlockFn(torch.autograd.Function):
         dA8 = None
         sparse = False
         if ds is not None:
-            if premasked:  # dout already masked + reduced by the next block's conv1 dgrad
-                g8a = q.grad_out(a_last, bn_l) if q is not None else None
-                g8b = q.grad_out(ad, ds[1]) if q is not None else None
+            if premasked and ctx.gram and fuse:
+                # bn3 in the Gram form (as for identity blocks below); the downsample BN alone gets an apply pass:
+                # its reductions (sum g, sum g xhat_d) sit in bn3's slab rows 1, 2 -> its own rows 1, 0
+                T = gram_T(dout, outs[-1]) if getattr(block, "_bnb_nox", False) else None
+                dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
+                C3, S = a_last.shape[-1], _lib.STAT_SLOTS  # (the BN-backward slab has the statistics slab's depth)
+                src = bn_l.work.scratch[: S * 3 * C3].view(S, 3, C3)
+                dst = ds[1].work.scratch[: S * 3 * C3].view(S, 3, C3)
+                dst[:, 0].copy_(src[:, 2])
+                dst[:, 1].copy_(src[:, 1])
+                dAd, _ = bn_apply_backward(dout, ad, None, ds[1], None, 1)
+                dAd8 = None
+            elif premasked:  # dout already masked + reduced by the next block's conv1 dgrad
+                g8a = q.grad_out(a_last, bn_l) if (q is not None and fp8_dgrad_ok(conv_l)) else None
+                g8b = q.grad_out(ad, ds[1]) if (q is not None and fp8_dgrad_ok(ds[0])) else None
                 dA, dAd = bn_apply_backward(dout, a_last, ad, bn_l, ds[1], 2, g8=(g8a, g8b))
                 dA8, dAd8 = _use8(q, g8a), _use8(q, g8b)
             else:
@@ -253,7 +287,7 @@ class BlockFn(torch.autograd.Function):
             dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
             dX = dout
         elif premasked:
-            g8a = q.grad_out(a_last, bn_l) if q is not None else None
+            g8a = q.grad_out(a_last, bn_l) if (q is not None and fp8_dgrad_ok(conv_l)) else None
             dA, _ = bn_apply_backward(dout, a_last, None, bn_l, None, 1, g8=(g8a, None))
             dA8 = _use8(q, g8a)
             dX = dout  # masked upstream gradient = identity-branch gradient; conv1 dgrad adds into it
@@ -283,7 +317,7 @@ class BlockFn(torch.autograd.Function):
                     _wgrad(conv, dA, h_in)
                 dA_w = dA
                 if fz is not None:
-                    g8a = q.grad_out(acts[i - 1], bn_prev) if q is not None else None
+                    g8a = q.grad_out(acts[i - 1], bn_prev) if (q is not None and fp8_dgrad_ok(pairs[i - 1][0])) else None
                     dA, _ = bn_apply_backward(dH, acts[i - 1], None, bn_prev, None, 0, g8=(g8a, None))
                     dA8 = _use8(q, g8a)
                 else:
@@ -302,7 +336,7 @@ class BlockFn(torch.autograd.Function):
                     pbn = prev.convs_bns()[-1][1]
                     pds = prev.downsample
                     # the previous block's bn3 backward takes the Gram form: sum(g xhat3) from g^T h2, x3 not read
-                    nox = _GRAM_NOX and getattr(prev, "_gram", False) and pds is None and pym is not None
+                    nox = _GRAM_NOX and getattr(prev, "_gram", False) and pym is not None
                     fz = BNBwdFuse(None if nox else pa, pbn, y=pym, x2=pad_,
                                    bn2=pds[1] if pds is not None else None)
                 if g_read is not None:

@@ -298,7 +298,7 @@ class BNBwdFuse:
         a.stats = w.scratch.data_ptr()
         # x None (with the mask bits): the epilogue never reads x; sum(g xhat) is then formed from g^T h2 by the
         # Gram-form bn3 backward (ops/bn_gram.py gram_coef with T)
-        assert self.x is not None or (self.y is not None and self.x2 is None), "BNBwdFuse without x: bits only"
+        assert self.x is not None or self.y is not None, "BNBwdFuse without x: the mask bits are required"
         a.bnx = _lib.ptr(self.x)
         assert self.y is None or self.y.dtype == torch.uint8, "BNBwdFuse.y: the ReLU mask bits"
         a.bnym = _lib.ptr(self.y)

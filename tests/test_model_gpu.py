@@ -170,7 +170,8 @@ def _fq(t, e):
 
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_fp8_forward_training_step(arch, monkeypatch):
-    """--dtype fp8 (e4m3 forward convs, bf16 backward).
+    """--dtype fp8: e4m3 forward convs where the 1-byte loop wins (ops.block.fp8_fwd_ok), e5m2 x e4m3 dgrads
+    where fp8_dgrad_ok, bf16 elsewhere.
 
     A quantised network is chaotic under ANY perturbation (an fp32 emulation of
     the same fake-quantisation moves ~20 % when merely run under bf16
@@ -190,7 +191,9 @@ def test_fp8_forward_training_step(arch, monkeypatch):
 
     def checked_fwd8(conv, h, h8, bn):
         y = orig(conv, h, h8, bn)
-        if h8 is not None:
+        if h8 is None:  # no e4m3 copy was written for this input: only for convs that run bf16
+            assert not blk.fp8_fwd_ok(conv) or conv is model.conv1, tuple(conv.weight.shape)
+        if h8 is not None and blk.fp8_fwd_ok(conv):
             ex, ew = int(h8[1].item()), int(conv.w8_exp.item())
             w = conv.weight.detach().float()
             assert ew == math.ceil(math.log2(w.abs().max().item() / 448.0))
@@ -220,7 +223,10 @@ def test_fp8_forward_training_step(arch, monkeypatch):
     st.arena.zero_grad()
     logits = model(x)
     F.cross_entropy(logits, lab).backward()
-    assert len(checked) == len(model.convs()) - 1  # every conv but the stem ran in fp8
+    # every conv the per-shape rule sends to fp8 ran in fp8 (ResNet-18 at 64x64: the 3x3 convs with >= 128
+    # input channels; ResNet-50 also its 1x1 convs with >= 512, or 256 into <= 128, input channels)
+    want = [c for c in model.convs() if c is not model.conv1 and blk.fp8_fwd_ok(c)]
+    assert want and len(checked) == len(want), (len(checked), len(want))
     l32 = ref(x[..., :3].float().permute(0, 3, 1, 2).contiguous())
     e_log = rel(logits, l32)
     print(f"fp8 {arch}: logits rel err vs fp32 {e_log:.3f}")
@@ -422,20 +428,26 @@ def test_fused_stem_pool_backward_matches_unfused():
     assert rel(b1, b0) < 1e-3
 
 
-def test_bn_gram_backward_matches_torch(monkeypatch):
-    """IMAGENT_BN_GRAM: every identity bottleneck whose backward is premasked (11 of ResNet-50's 16 blocks:
-    not the 4 downsample blocks, not the last one) takes bn3's backward without the apply pass -- conv3's
-    dgrad over [g | h2] with folded weights and bias, its wgrad from g^T h2, the Gram matrix h2^T h2 and
-    colsum(h2) (ops/bn_gram.py). Logits, every parameter gradient and the BN buffers against the fp32
-    PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward)."""
+@pytest.mark.parametrize("nox", [True, False], ids=["from_T", "from_slab"])
+def test_bn_gram_backward_matches_torch(monkeypatch, nox):
+    """IMAGENT_BN_GRAM: every bottleneck whose backward is premasked (15 of ResNet-50's 16 blocks: all but the
+    last, the 4 downsample blocks included) takes bn3's backward without its apply pass -- conv3's dgrad over
+    [g | h2] with folded weights and bias, its wgrad from g^T h2, the Gram matrix h2^T h2 and colsum(h2)
+    (ops/bn_gram.py); a downsample block keeps one apply pass for its downsample BN. ``from_T`` (default):
+    the next block's dgrad does not read x3 and bn3's sum(g xhat) comes from rowsum(W3 * g^T h2);
+    ``from_slab`` (IMAGENT_BN_GRAM=slab): from the dgrad epilogue's x3 read. Logits, every parameter gradient
+    and the BN buffers against the fp32 PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward)."""
     from imagent_amd.ops import block
     monkeypatch.setattr(block, "_GRAM", True)
+    monkeypatch.setattr(block, "_GRAM_NOX", nox)
     calls = []
-    real_d, real_w = block.gram_dgrad, block.gram_wgrad
+    real_d, real_w, real_t = block.gram_dgrad, block.gram_wgrad, block.gram_T
     monkeypatch.setattr(block, "gram_dgrad", lambda *a, **k: calls.append("d") or real_d(*a, **k))
     monkeypatch.setattr(block, "gram_wgrad", lambda *a, **k: calls.append("w") or real_w(*a, **k))
+    monkeypatch.setattr(block, "gram_T", lambda *a, **k: calls.append("t") or real_t(*a, **k))
     test_hip_vs_torch_forward_backward("resnet50", True)
-    assert calls.count("d") == 11 and calls.count("w") == 11, calls
+    assert calls.count("d") == 15 and calls.count("w") == 15, calls
+    assert calls.count("t") == (15 if nox else 0), calls
 
 
 @pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
