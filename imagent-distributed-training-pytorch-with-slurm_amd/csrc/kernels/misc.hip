@@ -733,6 +733,8 @@ IMK_EXPORT int imk_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, v
 
 IMK_EXPORT int imk_xent_fwd(const float* logits, const int64_t* labels, float* lse, float* loss_mean,
                             float* metrics, int B, int NC, float smoothing, void* stream) {
+    // the mean loss is accumulated by the blocks: cleared here (no separate fill launch by the caller)
+    if (hipMemsetAsync(loss_mean, 0, sizeof(float), (hipStream_t)stream) != hipSuccess) return -1;
     hipLaunchKernelGGL(xent_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits,
                        labels, lse, loss_mean, metrics, B, NC, smoothing);
     IMK_CHECK_LAUNCH();

@@ -124,7 +124,7 @@ class XentFn(torch.autograd.Function):
         logits = logits.contiguous()
         B, NC = logits.shape
         lse = torch.empty(B, device=logits.device, dtype=torch.float32)
-        loss = torch.zeros((), device=logits.device, dtype=torch.float32)
+        loss = torch.empty((), device=logits.device, dtype=torch.float32)  # cleared by imk_xent_fwd
         _lib.check(_lib.kernels().imk_xent_fwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(),
                                                loss.data_ptr(), _lib.ptr(metrics), B, NC,
                                                float(smoothing), _lib.stream_ptr()), "xent")
