@@ -150,7 +150,17 @@ class NativeState:
         S = _lib.STAT_SLOTS
         nbw = _lib.kernels().imk_bn_bwd_scratch_floats(1)
         per = [(2 * S + nbw) * c for c in sizes]        # stats slab + bwd slab/scratch (zeroed)
-        self.zero_ws = torch.zeros(sum(per), dtype=torch.float32, device=self.device)
+        # the Gram-form bn3 backward's accumulators per bottleneck (ops/bn_gram.py): T = g^T h2 [4p][p],
+        # G = h2^T h2 [p][p], colsum(h2) [p] -- zeroed with the slabs by the one per-step memset
+        gram = [(b, b.convs_bns()[-1][0]) for b in self.model.blocks() if len(b.convs_bns()) == 3]
+        gsz = [c3.out_channels * c3.in_channels + c3.in_channels * (c3.in_channels + 1) for _, c3 in gram]
+        self.zero_ws = torch.zeros(sum(per) + sum(gsz), dtype=torch.float32, device=self.device)
+        go = sum(per)
+        for (b, c3), n in zip(gram, gsz):
+            C4, p = c3.out_channels, c3.in_channels
+            w = self.zero_ws[go:go + n]
+            b._gram_ws = (w[:C4 * p].view(C4, p), w[C4 * p:C4 * p + p * p].view(p, p), w[C4 * p + p * p:])
+            go += n
         self.save_ws = torch.zeros(sum(4 * c for c in sizes), dtype=torch.float32, device=self.device)
         o = so = 0
         descs = (_lib.RunDesc * len(bns))()

@@ -65,6 +65,11 @@ _GRAM = os.environ.get("IMAGENT_BN_GRAM", "1") != "0"
 # with it, the next block's conv1 dgrad does not read x3 for bn3's sum(g xhat): x3 = h2 W3^T, so that sum is
 # rowsum(W3 * g^T h2) -- the weight gradient's GEMM (IMAGENT_BN_GRAM=slab: from the epilogue's x3 read, A/B)
 _GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
+# ... for blocks with at least this many output pixels (N x OH x OW): the form saves ~32 M p bytes of BatchNorm
+# traffic per block but costs two p x p x M GEMM extensions and ~8 small launches, so below ~10^5 pixels it
+# loses (same-box A/B: ResNet-152 at 256 img/GPU 4,699 img/s with every block in the Gram form vs 5,080 without,
+# at 1024 img/GPU 6,279 vs 6,019; ResNet-50 at 256 11,636 vs 12,097)
+_GRAM_MIN_ROWS = int(os.environ.get("IMAGENT_GRAM_MIN_ROWS", "100000"))
 
 
 def _gram_ok(block, q, x) -> bool:
@@ -75,8 +80,10 @@ def _gram_ok(block, q, x) -> bool:
     if not getattr(block, "_fuse_bnb", False):  # the next block's dgrad must reduce bn3 (premasked backward)
         return False
     c3 = pairs[-1][0]
+    s = pairs[1][0].stride  # the bottleneck's stride sits in conv2
+    rows = x.shape[0] * (x.shape[1] // s) * (x.shape[2] // s)
     return (c3.kh == 1 and c3.kw == 1 and c3.stride == 1 and c3.padding == 0 and c3.in_channels % 64 == 0
-            and c3.out_channels % 64 == 0)
+            and c3.out_channels % 64 == 0 and rows >= _GRAM_MIN_ROWS)
 
 
 def _xfuse_ok(conv, a, q) -> bool:
@@ -140,6 +147,12 @@ def _dg8(d8, conv):
     return (d8[0], d8[1], conv.wt8, conv.w8_exp)
 
 
+def _gws(block, i):
+    """Entry i (0 T, 1 G, 2 colsum) of the block's zeroed Gram workspace, or None (allocated on demand)."""
+    w = getattr(block, "_gram_ws", None)
+    return w[i] if w is not None else None
+
+
 def _wgrad(conv, dA, h):
     """``h`` is the conv's input, or (BN input, scale / shift) when the BN + ReLU before it is
     applied on the operand path (``IMAGENT_BN_XFUSE``)."""
@@ -183,7 +196,9 @@ class BlockFn(torch.autograd.Function):
                 continue
             q8 = q.out_for(a, q.slot[id(bn)]) if (q is not None and fp8_fwd_ok(pairs[i + 1][0])) else None
             if gram and i + 1 == len(pairs) - 1:
-                h2sum = torch.zeros(a.shape[-1], device=a.device, dtype=torch.float32)
+                gws = getattr(block, "_gram_ws", None)  # zeroed per step with the BN slabs (models/native.py)
+                h2sum = gws[2] if gws is not None else torch.zeros(a.shape[-1], device=a.device,
+                                                                    dtype=torch.float32)
             h = bn_act_forward(a, None, bn, None, 0, True, q8=q8, colsum=h2sum)
             h8 = (q8[0], q8[1]) if q8 is not None else None
             saved += [a, h]
@@ -256,7 +271,7 @@ class BlockFn(torch.autograd.Function):
             if premasked and ctx.gram and fuse:
                 # bn3 in the Gram form (as for identity blocks below); the downsample BN alone gets an apply pass:
                 # its reductions (sum g, sum g xhat_d) sit in bn3's slab rows 1, 2 -> its own rows 1, 0
-                T = gram_T(dout, outs[-1]) if getattr(block, "_bnb_nox", False) else None
+                T = gram_T(dout, outs[-1], out=_gws(block, 0)) if getattr(block, "_bnb_nox", False) else None
                 dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
                 C3, S = a_last.shape[-1], _lib.STAT_SLOTS  # (the BN-backward slab has the statistics slab's depth)
                 src = bn_l.work.scratch[: S * 3 * C3].view(S, 3, C3)
@@ -283,7 +298,7 @@ class BlockFn(torch.autograd.Function):
         elif premasked and ctx.gram and fuse:
             # dx3 kept as (g, A, B, c): no apply pass (ops/bn_gram.py); when the next block's dgrad ran without x3,
             # sum(g xhat3) comes from T = g^T h2 (formed here, reused by the weight gradient)
-            T = gram_T(dout, outs[-1]) if getattr(block, "_bnb_nox", False) else None
+            T = gram_T(dout, outs[-1], out=_gws(block, 0)) if getattr(block, "_bnb_nox", False) else None
             dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
             dX = dout
         elif premasked:
@@ -307,7 +322,7 @@ class BlockFn(torch.autograd.Function):
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 if isinstance(dA, GramBN):
                     dH = gram_dgrad(dA, conv, h_in, fz)
-                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum)  # issued now: it reads dout, which conv1's dgrad
+                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1))  # issued now: it reads dout, which conv1's dgrad
                 else:                                    # accumulates into below
                     dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))

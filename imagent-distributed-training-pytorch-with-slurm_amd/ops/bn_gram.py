@@ -33,10 +33,10 @@ class GramBN:
         self.g, self.coef, self.T = g, coef, T
 
 
-def gram_T(g: torch.Tensor, h2: torch.Tensor) -> torch.Tensor:
-    """T = g^T h2 [4p][p] fp32 (conv3's weight-gradient GEMM), on the current stream."""
+def gram_T(g: torch.Tensor, h2: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """T = g^T h2 [4p][p] fp32 (conv3's weight-gradient GEMM), on the current stream (``out``: zeroed)."""
     C4, p = g.shape[-1], h2.shape[-1]
-    T = torch.zeros((C4, p), device=g.device, dtype=torch.float32)
+    T = out if out is not None else torch.zeros((C4, p), device=g.device, dtype=torch.float32)
     igemm_wgrad(g, h2, T, 1, 0, 1, 1)
     return T
 
@@ -93,9 +93,10 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     return out
 
 
-def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None):
+def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: torch.Tensor = None):
     """conv3.weight.grad += A (g^T h2) + B (W3 h2^T h2) + c colsum(h2), on the wgrad side stream.
-    ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``).
+    ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``); ``G``: a zeroed
+    [p][p] fp32 accumulator (the per-step workspace) or None.
     Returns the side-stream event after the last read of ``g`` (or None without a side stream):
     the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
     side = streams.side_stream(h2.device) if h2.is_cuda else None
@@ -104,7 +105,8 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None):
     ctx = torch.cuda.stream(side) if side is not None else _Null()
     with ctx:
         C4, p = gb.g.shape[-1], h2.shape[-1]
-        G = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
+        if G is None:
+            G = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
         own_s = s is None
         if own_s:
             s = torch.zeros((p,), device=h2.device, dtype=torch.float32)

@@ -9,13 +9,14 @@ shift || true
 args=${@:---steps 3 --warmup 2}
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
-mkdir -p $R/gpurun_out/pmc
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $R/gpurun_out/pmc/p1 -o p1 --output-format rocpd \
+P=${PMC_DIR:-$R/gpurun_out/pmc}
+mkdir -p $P
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d $P/p1 -o p1 --output-format rocpd \
     -- python3 $R/bench.py $args
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES -d $R/gpurun_out/pmc/p2 -o p2 --output-format rocpd \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES -d $P/p2 -o p2 --output-format rocpd \
     -- python3 $R/bench.py $args
-timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS -d $R/gpurun_out/pmc/p3 -o p3 \
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS -d $P/p3 -o p3 \
     --output-format rocpd -- python3 $R/bench.py $args
 cd $R
-python3 scripts/pmc_summary.py $out $(ls gpurun_out/pmc/p1/*.db | head -1) $(ls gpurun_out/pmc/p2/*.db | head -1) \
-    $(ls gpurun_out/pmc/p3/*.db | head -1)
+python3 scripts/pmc_summary.py $out $(ls $P/p1/*.db | head -1) $(ls $P/p2/*.db | head -1) \
+    $(ls $P/p3/*.db | head -1)

@@ -440,6 +440,7 @@ def test_bn_gram_backward_matches_torch(monkeypatch, nox):
     from imagent_amd.ops import block
     monkeypatch.setattr(block, "_GRAM", True)
     monkeypatch.setattr(block, "_GRAM_NOX", nox)
+    monkeypatch.setattr(block, "_GRAM_MIN_ROWS", 0)  # every block, at this test's 16 x 64 x 64 input
     calls = []
     real_d, real_w, real_t = block.gram_dgrad, block.gram_wgrad, block.gram_T
     monkeypatch.setattr(block, "gram_dgrad", lambda *a, **k: calls.append("d") or real_d(*a, **k))
