@@ -114,7 +114,47 @@ __global__ __launch_bounds__(256) void bn_bwd_coef_T_kernel(const float* __restr
     coef[2 * C + o] = k0 - kx * mean;
 }
 
+// bn3's training statistics WITHOUT conv3's output (x3 = h2 W3^T, never written): per output channel o,
+//   mean = W3[o] . colsum(h2) / M,   E[x3^2] = W3[o] . (W3 G)[o] / M  (G = h2^T h2, P = W3 G),
+// var = E[x3^2] - mean^2 (biased, as the training BatchNorm normalises), -> stats [2][C] (mean, var; the running-
+// statistics update reads it), save [2][C] (mean, rstd; the backward), aff [2][C] (gamma rstd, beta - mean gamma
+// rstd; conv3's epilogue applies it). One wave per channel.
+__global__ __launch_bounds__(256) void bn_gram_fwd_stats_kernel(const bf16_t* __restrict__ w, const float* __restrict__ s,
+                                                                const float* __restrict__ P, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float* __restrict__ stats,
+                                                                float* __restrict__ save, float* __restrict__ aff, int C,
+                                                                int p, float inv_m, float eps) {
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (o >= C) return;  // wave-uniform
+    float m1 = 0.f, m2 = 0.f;
+    for (int i = lane; i < p; i += 64) {
+        const float wi = bf2f(w[(size_t)o * p + i]);
+        m1 += wi * s[i];
+        m2 += wi * P[(size_t)o * p + i];
+    }
+    m1 = wave_sum(m1) * inv_m;
+    m2 = wave_sum(m2) * inv_m;
+    if (lane) return;
+    const float var = fmaxf(m2 - m1 * m1, 0.f), rstd = rsqrtf(var + eps), sc = gamma[o] * rstd;
+    stats[o] = m1;
+    stats[C + o] = var;
+    save[o] = m1;
+    save[C + o] = rstd;
+    aff[o] = sc;
+    aff[C + o] = beta[o] - m1 * sc;
+}
+
 }  // namespace
+
+IMK_EXPORT int imk_bn_gram_fwd_stats(const void* w, const float* s, const float* P, const float* gamma,
+                                     const float* beta, float* stats, float* save, float* aff, long M, int C, int p,
+                                     float eps, void* stream) {
+    if (M <= 0 || C <= 0 || p <= 0) return -100;
+    hipLaunchKernelGGL(bn_gram_fwd_stats_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)w, s, P, gamma, beta, stats, save, aff, C, p, 1.f / (float)M, eps);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
 
 IMK_EXPORT int imk_bn_bwd_coef_T(const float* scratch, const float* T, const void* w, const float* save,
                                  const float* gamma, float* dgamma_acc, float* dbeta_acc, float* coef, long R, int C,

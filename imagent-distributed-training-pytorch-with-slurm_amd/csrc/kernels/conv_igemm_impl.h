@@ -113,6 +113,9 @@ struct IGemmArgs {
 #define IG_NOSTREAM 2048  // never the streaming short-K 1x1 kernel (conv_stream.hip; A/B testing)
 #define IG_ACCUM_SUB2 4096  // with IG_ACCUM: the old output is valid only at even (y, x) output pixels
                            // (a stride-2 1x1 dgrad wrote only that parity class, no memset); elsewhere 0
+#define IG_RES 8192   // (streaming 1x1 only) out = act(affine(acc) + bnx[e]): a residual read from bnx, not from Y
+#define IG_MASKOUT 16384  // (streaming 1x1 only, with IG_RELU) also write the ReLU mask of the stored output as bits
+                          // into bnym (byte e / 8, bit e % 8; bn.hip bn_fwd's `ym` format)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]
 
 static __device__ __attribute__((aligned(64))) uint32_t g_igemm_zero[16];  // zero line for masked DMA lanes (per TU)

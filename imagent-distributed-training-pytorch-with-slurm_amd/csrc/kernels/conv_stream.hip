@@ -110,6 +110,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     // plain epilogue: forward statistics (mean[] holds the shift: previous batch mean, or 0) and the eval
     // forward's folded BatchNorm (IG_AFFINE: a.bias = [scale | shift] -> sc / sh) + ReLU after the accumulate
     const bool affine = !bnb && (a.flags & IG_AFFINE), relu = !bnb && (a.flags & IG_RELU);
+    // IG_RES: the residual comes from bnx (training: a Gram-form block's bn3 + shortcut + ReLU in conv3's epilogue,
+    // ops/block.py), IG_MASKOUT: the ReLU mask of the stored output as bits (the next block's dgrad epilogue)
+    const bool resid = !bnb && (a.flags & IG_RES), maskout = relu && (a.flags & IG_MASKOUT);
     if (!bnb) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
@@ -223,6 +226,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 const int m = g * 16 + u * PPR + lane / CH;
                 e[u] = m < a.M ? (long)m * a.ldy + n : -1;
                 if (e[u] >= 0) {
+                    if (resid) oo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
                     if (accum) {
                         bool ok = true;
                         if (a.flags & IG_ACCUM_SUB2) {  // dense output grid: (oh, ow) of row m
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             v[2 * k] = fmaf(v[2 * k], sc[2 * k], sh[2 * k]);
                             v[2 * k + 1] = fmaf(v[2 * k + 1], sc[2 * k + 1], sh[2 * k + 1]);
                         }
-                        if (accum) {
+                        if (accum || resid) {
                             v[2 * k] += lo_bf(oo[q][k]);
                             v[2 * k + 1] += hi_bf(oo[q][k]);
                         }
@@ -312,6 +316,15 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
 #pragma unroll
                     for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
                     *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[q]) = o;
+                    if (maskout) {  // stored bf16 > 0: nonzero, sign clear, not NaN (as bn_fwd's ym)
+                        uint32_t b = 0;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const uint32_t h = (o[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                            b |= (h != 0u && h <= 0x7F80u ? 1u : 0u) << i;
+                        }
+                        const_cast<uint8_t*>(a.bnym)[e[q] >> 3] = (uint8_t)b;
+                    }
                     if (a.stats) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {  // statistics of the stored (bf16) values
@@ -401,6 +414,10 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     const bool eval_bn = a.flags & IG_AFFINE;
     if ((a.flags & IG_RELU) && !eval_bn) return 1;
     if (eval_bn && (a.stats || a.xbn || (a.flags & IG_BNBWD))) return 1;
+    if ((a.flags & (IG_RES | IG_MASKOUT)) &&
+        (!eval_bn || (a.flags & (IG_ACCUM | IG_BNBWD)) || ((a.flags & IG_RES) && !a.bnx) ||
+         ((a.flags & IG_MASKOUT) && (!a.bnym || !(a.flags & IG_RELU)))))
+        return -121;
     const bool has_bias = a.bias && !eval_bn;
     if (a.flags & IG_STEM) {  // 7x7 stem, C = 4, K = 7 x 32
         if (a.flags & (IG_OUT_F32 | IG_FP8 | IG_ACCUM | IG_BNBWD | IG_NOSTREAM)) return 1;

@@ -56,6 +56,7 @@ class NativeState:
             # nest every earlier block into this one's state_dict / parameters())
             object.__setattr__(b, "_prev_block", blocks[k - 1] if k > 0 else None)
             b._fuse_bnb = bnb_fusion
+            b._has_next = k + 1 < len(blocks)  # a next block whose conv1 dgrad finishes this block's last BN
             b._last_bn = None
             b._bnb_done = False
         self._bind_shadows()

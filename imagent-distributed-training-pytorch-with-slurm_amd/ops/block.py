@@ -33,7 +33,7 @@ import torch
 from . import _lib, streams
 from . import conv as _conv
 from .bn import bn_act_backward, bn_act_forward, bn_apply_backward, bn_scale_shift
-from .bn_gram import GramBN, gram_T, gram_coef, gram_dgrad, gram_wgrad
+from .bn_gram import GramBN, gram_T, gram_coef, gram_dgrad, gram_fwd_stats, gram_wgrad
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
@@ -70,6 +70,11 @@ _GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
 # loses (same-box A/B: ResNet-152 at 256 img/GPU 4,699 img/s with every block in the Gram form vs 5,080 without,
 # at 1024 img/GPU 6,279 vs 6,019; ResNet-50 at 256 11,636 vs 12,097)
 _GRAM_MIN_ROWS = int(os.environ.get("IMAGENT_GRAM_MIN_ROWS", "100000"))
+# ... and in identity blocks bn3's FORWARD too: its batch statistics come from h2 (mean = W3 colsum(h2) / M,
+# E[x3^2] = rowsum(W3 G * W3) / M with the Gram matrix G the weight gradient needs anyway), so conv3's epilogue
+# applies bn3 + shortcut + ReLU and writes the block output and its mask bits: x3 is never written or read
+# (IMAGENT_BN_GRAM_FWD=0: off, A/B)
+_GRAM_FWD = os.environ.get("IMAGENT_BN_GRAM_FWD", "1") != "0"
 
 
 def _gram_ok(block, q, x) -> bool:
@@ -203,17 +208,35 @@ class BlockFn(torch.autograd.Function):
             h8 = (q8[0], q8[1]) if q8 is not None else None
             saved += [a, h]
         conv, bn, _ = pairs[-1]
-        if ss is not None:
+        fuse_next = getattr(block, "_fuse_bnb", False)
+        # the block output's e4m3 copy only when the next block's conv1 or downsample conv reads fp8
+        need8 = q is not None and getattr(block, "_q8_out", True)
+        gws = getattr(block, "_gram_ws", None)
+        # bn3 + shortcut + ReLU in conv3's epilogue (x3 never materialised): an identity Gram-form block whose
+        # output mask the next block's x-free dgrad epilogue reads, conv3 on the streaming kernel
+        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and ds is None and fuse_next and not need8
+                  and getattr(block, "_has_next", False) and gws is not None
+                  and h2sum is not None and conv.in_channels in (64, 128, 256) and x.shape[-1] == conv.out_channels)
+        gram_P = None
+        if fused3:
+            aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1])
+            out = torch.empty_like(x)
+            # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue
+            ym = torch.empty(out.numel() // 8, device=out.device, dtype=torch.uint8)
+            igemm_fwd(h, conv.w_bf16, 1, 0, 1, 1, out=out, affine=aff, relu=True, res=x, maskout=ym)
+            a = None
+        elif ss is not None:
             a = igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
         else:
             a = _fwd8(conv, h, h8, bn)
-        # the block output's e4m3 copy only when the next block's conv1 or downsample conv reads fp8
-        q8 = q.out_for(a, q.slot[id(bn)]) if (q is not None and getattr(block, "_q8_out", True)) else None
-        # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue (1/16
-        # of the bytes of re-reading the output there)
-        fuse_next = getattr(block, "_fuse_bnb", False)
-        ym = torch.empty(a.numel() // 8, device=a.device, dtype=torch.uint8) if fuse_next else None
-        if ds is not None:
+        q8 = q.out_for(a, q.slot[id(bn)]) if (need8 and a is not None) else None
+        if not fused3:
+            # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue (1/16
+            # of the bytes of re-reading the output there)
+            ym = torch.empty(a.numel() // 8, device=a.device, dtype=torch.uint8) if fuse_next else None
+        if fused3:
+            ad = None
+        elif ds is not None:
             if side is not None:
                 cur = torch.cuda.current_stream()
                 cur.wait_stream(side)
@@ -228,7 +251,7 @@ class BlockFn(torch.autograd.Function):
             q.register(out, q8)
         saved += [a, ad, out]
         # rows seen by each BN (module order: bn1..bnK, downsample.1) for the running-stat update
-        rows = [t.numel() // t.shape[-1] for t in saved[1:-3:2]] + [a.numel() // a.shape[-1]]
+        rows = [t.numel() // t.shape[-1] for t in saved[1:-3:2]] + [out.numel() // out.shape[-1]]
         if ad is not None:
             rows.append(ad.numel() // ad.shape[-1])
         block._bn_rows = rows
@@ -239,6 +262,7 @@ class BlockFn(torch.autograd.Function):
         ctx.xbn = xbn
         ctx.gram = gram
         ctx.h2sum = h2sum
+        ctx.gram_P = gram_P  # W3 G from the fused forward (G in the block's workspace): not recomputed
         block._gram = gram  # the next block's conv1 dgrad may then skip reading x3 (BNBwdFuse without x)
         block._bnb_nox = False
         ctx.save_for_backward(*saved)
@@ -322,7 +346,7 @@ class BlockFn(torch.autograd.Function):
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 if isinstance(dA, GramBN):
                     dH = gram_dgrad(dA, conv, h_in, fz)
-                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1))  # issued now: it reads dout, which conv1's dgrad
+                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1), P=ctx.gram_P)  # issued now: it reads dout, which conv1's dgrad
                 else:                                    # accumulates into below
                     dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))

@@ -93,10 +93,29 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     return out
 
 
-def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: torch.Tensor = None):
+def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor):
+    """bn3's batch statistics without conv3's output (x3 = h2 W3^T): G = h2^T h2 into the zeroed ``G``, P =
+    W3 G, then mean = W3 s / M, E[x3^2] = rowsum(P * W3) / M (``bn_gram_fwd_stats_kernel``) into ``bn.work.stats``
+    / ``save``. Returns (aff [2][4p] = (gamma rstd, beta - mean gamma rstd) for conv3's epilogue, P; the weight
+    gradient reuses G and P)."""
+    C4, p = conv.out_channels, conv.in_channels
+    igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
+    P = torch.mm(conv.w_bf16.view(C4, p).float(), G)
+    aff = torch.empty((2, C4), device=h2.device, dtype=torch.float32)
+    w = bn.work
+    _lib.check(_lib.kernels().imk_bn_gram_fwd_stats(conv.w_bf16.data_ptr(), s.data_ptr(), P.data_ptr(),
+                                                    bn.weight.data_ptr(), bn.bias.data_ptr(), w.stats.data_ptr(),
+                                                    w.save.data_ptr(), aff.data_ptr(), h2.numel() // p, C4, p,
+                                                    float(bn.eps), _lib.stream_ptr()), "bn gram fwd stats")
+    return aff, P
+
+
+def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: torch.Tensor = None,
+               P: torch.Tensor = None):
     """conv3.weight.grad += A (g^T h2) + B (W3 h2^T h2) + c colsum(h2), on the wgrad side stream.
     ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``); ``G``: a zeroed
-    [p][p] fp32 accumulator (the per-step workspace) or None.
+    [p][p] fp32 accumulator (the per-step workspace) or None; ``P`` = W3 G when the forward already formed G
+    and P (``gram_fwd_stats``): then neither is recomputed.
     Returns the side-stream event after the last read of ``g`` (or None without a side stream):
     the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
     side = streams.side_stream(h2.device) if h2.is_cuda else None
@@ -105,7 +124,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
     ctx = torch.cuda.stream(side) if side is not None else _Null()
     with ctx:
         C4, p = gb.g.shape[-1], h2.shape[-1]
-        if G is None:
+        if G is None and P is None:
             G = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
         own_s = s is None
         if own_s:
@@ -118,16 +137,18 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record(side)
-        igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
+        if P is None:
+            igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
         if own_s:
             colsum_into(h2.view(-1, p), s)
-        P = torch.mm(conv.w_bf16.view(C4, p).float(), G)  # W3 G [4p][p]
+        if P is None:
+            P = torch.mm(conv.w_bf16.view(C4, p).float(), G)  # W3 G [4p][p]
         _lib.check(_lib.kernels().imk_bn_gram_wgrad_fixup(conv.weight.grad.data_ptr(), T.data_ptr(), P.data_ptr(),
                                                           gb.coef.data_ptr(), s.data_ptr(), C4, p,
                                                           _lib.stream_ptr()), "gram wgrad fixup")
         notify_ready(conv.weight)
     if side is not None:
-        streams.protect(gb.g, gb.coef, h2, s, T)
+        streams.protect(*[t for t in (gb.g, gb.coef, h2, s, T, P) if t is not None])
         streams.ensure_join_after_backward()
     return ev
 

@@ -140,7 +140,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
               out_f32: bool = False, relu: bool = False, out: Optional[torch.Tensor] = None,
               tile: int = 0, stem: bool = False, epi: int = 0,
               fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, affine: Optional[torch.Tensor] = None,
-              accumulate: bool = False, xbn: Optional[torch.Tensor] = None) -> torch.Tensor:
+              accumulate: bool = False, xbn: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
+              maskout: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` (a [STAT_SLOTS, 2, Co]
     slab), or, given a BatchNorm workspace (``bn.work``), into its slab as
@@ -156,7 +157,10 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     the epilogue (before ``accumulate`` into ``out`` and ``relu``).
     ``xbn`` [2, Ci] fp32 (scale, shift): the operand is relu(x * scale + shift) -- the producing
     BatchNorm's apply + ReLU done on this conv's operand load (1x1, Ci in {64, 128}: the
-    streaming kernel; see :func:`ops.bn.bn_scale_shift`)."""
+    streaming kernel; see :func:`ops.bn.bn_scale_shift`).
+    ``res`` (like ``out``): added after ``affine`` and before ``relu`` (training: a block's last BatchNorm +
+    shortcut + ReLU in the conv's epilogue); ``maskout`` (uint8, numel / 8): also the ReLU mask of the stored
+    output as bits. Both: the streaming 1x1 kernel only."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
@@ -176,6 +180,14 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
         assert bias is None and affine.shape == (2, Co) and affine.dtype == torch.float32
         a.flags |= 1024
         a.bias = affine.data_ptr()
+    if res is not None:
+        assert res.shape == out.shape and res.dtype == torch.bfloat16 and res.is_contiguous()
+        a.flags |= 8192
+        a.bnx = res.data_ptr()
+    if maskout is not None:
+        assert maskout.dtype == torch.uint8 and maskout.numel() * 8 == out.numel() and relu
+        a.flags |= 16384
+        a.bnym = maskout.data_ptr()
     if fp8 is not None:
         assert x.dtype == torch.uint8 and w.dtype == torch.uint8, (x.dtype, w.dtype)
         a.flags |= 256

@@ -428,20 +428,26 @@ def test_fused_stem_pool_backward_matches_unfused():
     assert rel(b1, b0) < 1e-3
 
 
-@pytest.mark.parametrize("nox", [True, False], ids=["from_T", "from_slab"])
-def test_bn_gram_backward_matches_torch(monkeypatch, nox):
+@pytest.mark.parametrize("nox,fwd", [(True, True), (True, False), (False, False)],
+                         ids=["from_T_fused_fwd", "from_T", "from_slab"])
+def test_bn_gram_backward_matches_torch(monkeypatch, nox, fwd):
     """IMAGENT_BN_GRAM: every bottleneck whose backward is premasked (15 of ResNet-50's 16 blocks: all but the
     last, the 4 downsample blocks included) takes bn3's backward without its apply pass -- conv3's dgrad over
     [g | h2] with folded weights and bias, its wgrad from g^T h2, the Gram matrix h2^T h2 and colsum(h2)
     (ops/bn_gram.py); a downsample block keeps one apply pass for its downsample BN. ``from_T`` (default):
     the next block's dgrad does not read x3 and bn3's sum(g xhat) comes from rowsum(W3 * g^T h2);
     ``from_slab`` (IMAGENT_BN_GRAM=slab): from the dgrad epilogue's x3 read. Logits, every parameter gradient
-    and the BN buffers against the fp32 PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward)."""
+    and the BN buffers against the fp32 PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward).
+    ``from_T_fused_fwd`` (IMAGENT_BN_GRAM_FWD, default): the 10 identity blocks with a next block and p <= 256 take bn3's
+    forward from h2 (statistics from W3, colsum(h2) and h2^T h2) with bn3 + shortcut + ReLU in conv3's epilogue."""
     from imagent_amd.ops import block
     monkeypatch.setattr(block, "_GRAM", True)
     monkeypatch.setattr(block, "_GRAM_NOX", nox)
     monkeypatch.setattr(block, "_GRAM_MIN_ROWS", 0)  # every block, at this test's 16 x 64 x 64 input
+    monkeypatch.setattr(block, "_GRAM_FWD", fwd)
     calls = []
+    real_f = block.gram_fwd_stats
+    monkeypatch.setattr(block, "gram_fwd_stats", lambda *a, **k: calls.append("f") or real_f(*a, **k))
     real_d, real_w, real_t = block.gram_dgrad, block.gram_wgrad, block.gram_T
     monkeypatch.setattr(block, "gram_dgrad", lambda *a, **k: calls.append("d") or real_d(*a, **k))
     monkeypatch.setattr(block, "gram_wgrad", lambda *a, **k: calls.append("w") or real_w(*a, **k))
@@ -449,6 +455,7 @@ def test_bn_gram_backward_matches_torch(monkeypatch, nox):
     test_hip_vs_torch_forward_backward("resnet50", True)
     assert calls.count("d") == 15 and calls.count("w") == 15, calls
     assert calls.count("t") == (15 if nox else 0), calls
+    assert calls.count("f") == (10 if fwd else 0), calls
 
 
 @pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
