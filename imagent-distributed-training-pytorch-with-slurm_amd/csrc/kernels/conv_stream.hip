@@ -112,13 +112,18 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     const bool affine = !bnb && (a.flags & IG_AFFINE), relu = !bnb && (a.flags & IG_RELU);
     // IG_RES: the residual comes from bnx (training: a Gram-form block's bn3 + shortcut + ReLU in conv3's epilogue,
     // ops/block.py), IG_MASKOUT: the ReLU mask of the stored output as bits (the next block's dgrad epilogue)
+    // (bnsave2 non-null with IG_RES: a per-channel scale on the residual, a downsample block's shortcut BN whose
+    // shift the caller folded into bias[Nout..])
     const bool resid = !bnb && (a.flags & IG_RES), maskout = relu && (a.flags & IG_MASKOUT);
+    const bool resaff = resid && a.bnsave2;
+    float rsc[8];
     if (!bnb) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             mean[c] = (a.stats && a.shift) ? a.shift[n + c] : 0.f;
             sc[c] = affine ? a.bias[n + c] : 1.f;
             sh[c] = affine ? a.bias[a.Nout + n + c] : 0.f;
+            rsc[c] = resaff ? a.bnsave2[n + c] : 1.f;
         }
     }
     float s1[8], s2[8], s3[8];
@@ -290,7 +295,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             v[2 * k] = fmaf(v[2 * k], sc[2 * k], sh[2 * k]);
                             v[2 * k + 1] = fmaf(v[2 * k + 1], sc[2 * k + 1], sh[2 * k + 1]);
                         }
-                        if (accum || resid) {
+                        if (resaff) {
+                            v[2 * k] = fmaf(lo_bf(oo[q][k]), rsc[2 * k], v[2 * k]);
+                            v[2 * k + 1] = fmaf(hi_bf(oo[q][k]), rsc[2 * k + 1], v[2 * k + 1]);
+                        } else if (accum || resid) {
                             v[2 * k] += lo_bf(oo[q][k]);
                             v[2 * k + 1] += hi_bf(oo[q][k]);
                         }

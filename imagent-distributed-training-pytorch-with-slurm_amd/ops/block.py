@@ -212,18 +212,30 @@ class BlockFn(torch.autograd.Function):
         # the block output's e4m3 copy only when the next block's conv1 or downsample conv reads fp8
         need8 = q is not None and getattr(block, "_q8_out", True)
         gws = getattr(block, "_gram_ws", None)
-        # bn3 + shortcut + ReLU in conv3's epilogue (x3 never materialised): an identity Gram-form block whose
-        # output mask the next block's x-free dgrad epilogue reads, conv3 on the streaming kernel
-        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and ds is None and fuse_next and not need8
-                  and getattr(block, "_has_next", False) and gws is not None
-                  and h2sum is not None and conv.in_channels in (64, 128, 256) and x.shape[-1] == conv.out_channels)
+        # bn3 + shortcut + ReLU in conv3's epilogue (x3 never materialised): a Gram-form block whose output mask
+        # the next block's x-free dgrad epilogue reads, conv3 on the streaming kernel. A downsample block's
+        # shortcut BN enters as a per-channel scale on the residual (its shift folded into bn3's)
+        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and fuse_next and not need8
+                  and getattr(block, "_has_next", False) and gws is not None and h2sum is not None
+                  and conv.in_channels in (64, 128, 256) and (ds is not None or x.shape[-1] == conv.out_channels))
         gram_P = None
         if fused3:
             aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1])
-            out = torch.empty_like(x)
+            res, rsc = x, None
+            if ds is not None:
+                if side is not None:
+                    cur = torch.cuda.current_stream()
+                    cur.wait_stream(side)
+                    ad.record_stream(cur)
+                else:
+                    ad = _fwd8(ds[0], x, x8, ds[1])
+                ssd = bn_scale_shift(ad, ds[1])
+                aff[1] += ssd[1]
+                res, rsc = ad, ssd[0]
+            out = torch.empty(res.shape, device=res.device, dtype=res.dtype)
             # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue
             ym = torch.empty(out.numel() // 8, device=out.device, dtype=torch.uint8)
-            igemm_fwd(h, conv.w_bf16, 1, 0, 1, 1, out=out, affine=aff, relu=True, res=x, maskout=ym)
+            igemm_fwd(h, conv.w_bf16, 1, 0, 1, 1, out=out, affine=aff, relu=True, res=res, maskout=ym, res_scale=rsc)
             a = None
         elif ss is not None:
             a = igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
@@ -235,7 +247,7 @@ class BlockFn(torch.autograd.Function):
             # of the bytes of re-reading the output there)
             ym = torch.empty(a.numel() // 8, device=a.device, dtype=torch.uint8) if fuse_next else None
         if fused3:
-            ad = None
+            pass
         elif ds is not None:
             if side is not None:
                 cur = torch.cuda.current_stream()
@@ -297,7 +309,7 @@ class BlockFn(torch.autograd.Function):
                 # its reductions (sum g, sum g xhat_d) sit in bn3's slab rows 1, 2 -> its own rows 1, 0
                 T = gram_T(dout, outs[-1], out=_gws(block, 0)) if getattr(block, "_bnb_nox", False) else None
                 dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
-                C3, S = a_last.shape[-1], _lib.STAT_SLOTS  # (the BN-backward slab has the statistics slab's depth)
+                C3, S = out.shape[-1], _lib.STAT_SLOTS  # (the BN-backward slab has the statistics slab's depth)
                 src = bn_l.work.scratch[: S * 3 * C3].view(S, 3, C3)
                 dst = ds[1].work.scratch[: S * 3 * C3].view(S, 3, C3)
                 dst[:, 0].copy_(src[:, 2])

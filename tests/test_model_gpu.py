@@ -438,8 +438,9 @@ def test_bn_gram_backward_matches_torch(monkeypatch, nox, fwd):
     the next block's dgrad does not read x3 and bn3's sum(g xhat) comes from rowsum(W3 * g^T h2);
     ``from_slab`` (IMAGENT_BN_GRAM=slab): from the dgrad epilogue's x3 read. Logits, every parameter gradient
     and the BN buffers against the fp32 PyTorch model, as the unfused path (test_hip_vs_torch_forward_backward).
-    ``from_T_fused_fwd`` (IMAGENT_BN_GRAM_FWD, default): the 10 identity blocks with a next block and p <= 256 take bn3's
-    forward from h2 (statistics from W3, colsum(h2) and h2^T h2) with bn3 + shortcut + ReLU in conv3's epilogue."""
+    ``from_T_fused_fwd`` (IMAGENT_BN_GRAM_FWD, default): the 13 blocks with a next block and p <= 256 (the 3
+    downsample blocks among them) take bn3's forward from h2 (statistics from W3, colsum(h2) and h2^T h2) with
+    bn3 + shortcut (+ the shortcut's BN as a residual scale) + ReLU in conv3's epilogue."""
     from imagent_amd.ops import block
     monkeypatch.setattr(block, "_GRAM", True)
     monkeypatch.setattr(block, "_GRAM_NOX", nox)
@@ -455,7 +456,7 @@ def test_bn_gram_backward_matches_torch(monkeypatch, nox, fwd):
     test_hip_vs_torch_forward_backward("resnet50", True)
     assert calls.count("d") == 15 and calls.count("w") == 15, calls
     assert calls.count("t") == (15 if nox else 0), calls
-    assert calls.count("f") == (10 if fwd else 0), calls
+    assert calls.count("f") == (13 if fwd else 0), calls
 
 
 @pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
