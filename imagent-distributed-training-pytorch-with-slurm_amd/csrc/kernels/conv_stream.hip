@@ -250,7 +250,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     }
                 }
             };
-            if (bnb) {
+            // the epilogue's global reads go out before the MFMAs whenever there are any (BN-backward x / mask,
+            // the accumulated old output, the residual): their latency hides behind the group's MFMAs
+            const bool early = bnb || accum || resid;
+            if (early) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u) issue(u);
             }
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             // (2) coalesced row chunks: pixel q*PPR + lane/CH, channels n .. n+7
 #pragma unroll
             for (int q0 = 0; q0 < NR; q0 += QB) {
-                if (!bnb) {
+                if (!early) {
 #pragma unroll
                     for (int u = 0; u < QB; ++u) issue(q0 + u);
                 }
