@@ -160,7 +160,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         const int r = conv_stream(a, st, bn_hint);
         if (r != 1) return r;
     }
-    if (a.flags & (IG_RES | IG_MASKOUT)) return -121;  // only the streaming kernel has that epilogue
+    if (a.flags & (IG_RES | IG_MASKOUT | IG_Q8OUT)) return -121;  // only the streaming kernel has that epilogue
     if (autotile) tile = (a.Nout <= 64) ? 4 : 2;
     // measured on MI355X (profiles/r50_conv_layers_*): the register-staged
     // pipeline wins for 64-wide output tiles and single-stage (K <= 64) tiles,

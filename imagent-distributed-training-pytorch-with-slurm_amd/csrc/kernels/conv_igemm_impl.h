@@ -97,6 +97,11 @@ struct IGemmArgs {
     // the sums before the mask (bn_gram.hip: the bottleneck's bn3 backward folded into conv3's dgrad)
     const bf16_t* X2;
     int C2;
+    // IG_Q8OUT (streaming 1x1 only): also the e4m3 copy of the stored bf16 output for fp8 consumers, quantised
+    // with 2^-y8exp[0] (delayed scaling, fp8.hip), |y| max into y8amax[blockIdx & 31] (as bn_fwd's y8)
+    void* Y8;
+    const int* y8exp;
+    float* y8amax;
 };
 
 #define IG_OUT_F32 1   // fp32 output (else bf16)
@@ -114,6 +119,7 @@ struct IGemmArgs {
 #define IG_ACCUM_SUB2 4096  // with IG_ACCUM: the old output is valid only at even (y, x) output pixels
                            // (a stride-2 1x1 dgrad wrote only that parity class, no memset); elsewhere 0
 #define IG_RES 8192   // (streaming 1x1 only) out = act(affine(acc) + bnx[e]): a residual read from bnx, not from Y
+#define IG_Q8OUT 32768  // (streaming 1x1 only) also the e4m3 copy of the output (Y8 / y8exp / y8amax)
 #define IG_MASKOUT 16384  // (streaming 1x1 only, with IG_RELU) also write the ReLU mask of the stored output as bits
                           // into bnym (byte e / 8, bit e % 8; bn.hip bn_fwd's `ym` format)
 #define STAT_SLOTS 32  // stats slab: [STAT_SLOTS][2][Nout]

@@ -35,7 +35,9 @@
 namespace {
 
 // MODE 0: plain epilogue (+ optional IG_ACCUM); IG_BNBWD with the ReLU mask
-// from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3)
+// from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3); 4: the plain epilogue with
+// a training block's fused output (IG_RES residual (+ scale), IG_MASKOUT mask bits, IG_Q8OUT e4m3 copy) -- a
+// mode of its own so that the registers of those paths never weigh on the plain kernels (eval, forward convs)
 // STEM: the 7x7/2 stem as a row-segment gather (C = 4 padded channels, a
 // kernel row = 8 taps x 4 channels = 32 K elements, K = KH x 32): one MFMA
 // k-step per kernel row, the lane's B fragment = 2 taps x 4 channels = two
@@ -54,7 +56,8 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     constexpr int CH = BN / 8;        // 16-B output chunks per pixel
     constexpr int PPR = 64 / CH;      // pixels per epilogue read instruction
     constexpr int NR = 16 / PPR;      // epilogue reads per 16-pixel group
-    constexpr bool bnb = MODE != 0, has_y = MODE == 1 || MODE == 3, has_x2 = MODE == 3;
+    constexpr bool bnb = MODE >= 1 && MODE <= 3, has_y = MODE == 1 || MODE == 3, has_x2 = MODE == 3;
+    constexpr bool FO = MODE == 4;
     // chunks whose global reads are batched; with the BN-backward epilogue all
     // of a group's reads (x, y | x2, old) are issued before its MFMAs
     constexpr int QB = bnb ? NR : (NR < 4 ? NR : 4);
@@ -114,8 +117,12 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     // ops/block.py), IG_MASKOUT: the ReLU mask of the stored output as bits (the next block's dgrad epilogue)
     // (bnsave2 non-null with IG_RES: a per-channel scale on the residual, a downsample block's shortcut BN whose
     // shift the caller folded into bias[Nout..])
-    const bool resid = !bnb && (a.flags & IG_RES), maskout = relu && (a.flags & IG_MASKOUT);
+    const bool resid = FO && (a.flags & IG_RES), maskout = FO && relu && (a.flags & IG_MASKOUT);
     const bool resaff = resid && a.bnsave2;
+    // IG_Q8OUT: the e4m3 copy of the stored output (delayed-scaled, amax-tracked) for an fp8 consumer
+    const bool q8out = FO && (a.flags & IG_Q8OUT);
+    const float q8s = q8out ? ldexpf(1.f, -a.y8exp[0]) : 0.f;
+    float m8 = 0.f;
     float rsc[8];
     if (!bnb) {
 #pragma unroll
@@ -250,9 +257,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     }
                 }
             };
-            // the epilogue's global reads go out before the MFMAs whenever there are any (BN-backward x / mask,
-            // the accumulated old output, the residual): their latency hides behind the group's MFMAs
-            const bool early = bnb || accum || resid;
+            // the BN-backward (x / mask) and residual reads go out before the MFMAs: their latency hides behind
+            // the group's MFMAs (the accumulated old output too measured slower: eval 52.8k -> 48.9k val img/s,
+            // deterministic 11.7k -> 11.2k img/s)
+            const bool early = bnb || resid;
             if (early) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u) issue(u);
@@ -327,6 +335,19 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
 #pragma unroll
                     for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
                     *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[q]) = o;
+                    if (q8out) {  // quantise the bf16-rounded values the bf16 consumers see
+                        float w[8];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            w[2 * k] = lo_bf(o[k]);
+                            w[2 * k + 1] = hi_bf(o[k]);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) m8 = fmaxf(m8, fabsf(w[i]));
+                        *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(a.Y8) + e[q]) =
+                            u32x2{pack4_fp8(w[0] * q8s, w[1] * q8s, w[2] * q8s, w[3] * q8s),
+                                  pack4_fp8(w[4] * q8s, w[5] * q8s, w[6] * q8s, w[7] * q8s)};
+                    }
                     if (maskout) {  // stored bf16 > 0: nonzero, sign clear, not NaN (as bn_fwd's ym)
                         uint32_t b = 0;
 #pragma unroll
@@ -369,6 +390,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             __builtin_amdgcn_wave_barrier();
         }
     }
+    if (q8out) {  // one atomic per wave into the 32-slot amax row
+        m8 = wave_max(m8);
+        if (lane == 0) atomic_max_pos(a.y8amax + (blockIdx.x & 31), m8);
+    }
     if (!a.stats) return;
     // fold the lanes that share a channel chunk, one atomic per channel and quantity
 #pragma unroll
@@ -407,8 +432,14 @@ int launch_stream1(const IGemmArgs& a, hipStream_t st) {
 }
 
 template <int K, int BN, int D>
+int launch_plain(const IGemmArgs& a, hipStream_t st) {
+    if (a.flags & (IG_RES | IG_MASKOUT | IG_Q8OUT)) return launch_stream1<K, BN, D, 4>(a, st);
+    return launch_stream1<K, BN, D, 0>(a, st);
+}
+
+template <int K, int BN, int D>
 int launch_stream(const IGemmArgs& a, hipStream_t st) {
-    if (!(a.flags & IG_BNBWD)) return launch_stream1<K, BN, D, 0>(a, st);
+    if (!(a.flags & IG_BNBWD)) return launch_plain<K, BN, D>(a, st);
     if constexpr (BN <= 128) {
         if (a.bnx2) return a.bnym ? launch_stream1<K, BN, D, 3>(a, st) : 1;
         return a.bnym ? launch_stream1<K, BN, D, 1>(a, st) : launch_stream1<K, BN, D, 2>(a, st);
@@ -425,9 +456,10 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     const bool eval_bn = a.flags & IG_AFFINE;
     if ((a.flags & IG_RELU) && !eval_bn) return 1;
     if (eval_bn && (a.stats || a.xbn || (a.flags & IG_BNBWD))) return 1;
-    if ((a.flags & (IG_RES | IG_MASKOUT)) &&
-        (!eval_bn || (a.flags & (IG_ACCUM | IG_BNBWD)) || ((a.flags & IG_RES) && !a.bnx) ||
-         ((a.flags & IG_MASKOUT) && (!a.bnym || !(a.flags & IG_RELU)))))
+    if ((a.flags & (IG_RES | IG_MASKOUT | IG_Q8OUT)) &&
+        (!eval_bn || (a.flags & (IG_ACCUM | IG_BNBWD | IG_STEM)) || ((a.flags & IG_RES) && !a.bnx) ||
+         ((a.flags & IG_MASKOUT) && (!a.bnym || !(a.flags & IG_RELU))) ||
+         ((a.flags & IG_Q8OUT) && (!a.Y8 || !a.y8exp || !a.y8amax))))
         return -121;
     const bool has_bias = a.bias && !eval_bn;
     if (a.flags & IG_STEM) {  // 7x7 stem, C = 4, K = 7 x 32
@@ -460,7 +492,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // fwd 264 vs 370).
     if (!(a.flags & IG_BNBWD) && a.C == 256 && a.Nout > 128) {
         if (bn != 0 && bn != 64) return 1;
-        return launch_stream1<256, 64, 2, 0>(a, st);
+        return launch_plain<256, 64, 2>(a, st);
     }
     int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (a.flags & IG_BNBWD) {
@@ -511,7 +543,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // K = 256 into <= 128 channels (bottleneck conv1 256 -> 64 / 128): 64-channel
     // slices, plain epilogue
     if (a.C == 256 && a.Nout <= 128) {
-        if (!(a.flags & IG_BNBWD)) return launch_stream1<256, 64, 2, 0>(a, st);
+        if (!(a.flags & IG_BNBWD)) return launch_plain<256, 64, 2>(a, st);
         if (!a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
     }
     return 1;

@@ -89,6 +89,7 @@ class IGemmArgs(C.Structure):
         ("xexp", C.c_void_p), ("wexp", C.c_void_p), ("shift", C.c_void_p),
         ("xbn", C.c_void_p),
         ("X2", C.c_void_p), ("C2", C.c_int),
+        ("Y8", C.c_void_p), ("y8exp", C.c_void_p), ("y8amax", C.c_void_p),
     ]
 
 

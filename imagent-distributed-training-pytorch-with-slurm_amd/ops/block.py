@@ -215,7 +215,7 @@ class BlockFn(torch.autograd.Function):
         # bn3 + shortcut + ReLU in conv3's epilogue (x3 never materialised): a Gram-form block whose output mask
         # the next block's x-free dgrad epilogue reads, conv3 on the streaming kernel. A downsample block's
         # shortcut BN enters as a per-channel scale on the residual (its shift folded into bn3's)
-        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and fuse_next and not need8
+        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and fuse_next
                   and getattr(block, "_has_next", False) and gws is not None and h2sum is not None
                   and conv.in_channels in (64, 128, 256) and (ds is not None or x.shape[-1] == conv.out_channels))
         gram_P = None
@@ -233,16 +233,19 @@ class BlockFn(torch.autograd.Function):
                 aff[1] += ssd[1]
                 res, rsc = ad, ssd[0]
             out = torch.empty(res.shape, device=res.device, dtype=res.dtype)
-            # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue
+            # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue; the output's
+            # e4m3 copy from the same epilogue when an fp8 conv reads it
             ym = torch.empty(out.numel() // 8, device=out.device, dtype=torch.uint8)
-            igemm_fwd(h, conv.w_bf16, 1, 0, 1, 1, out=out, affine=aff, relu=True, res=res, maskout=ym, res_scale=rsc)
+            q8 = q.out_for(out, q.slot[id(bn)]) if need8 else None
+            igemm_fwd(h, conv.w_bf16, 1, 0, 1, 1, out=out, affine=aff, relu=True, res=res, maskout=ym, res_scale=rsc,
+                      q8out=q8)
             a = None
         elif ss is not None:
             a = igemm_fwd(h, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, xbn=ss)
         else:
             a = _fwd8(conv, h, h8, bn)
-        q8 = q.out_for(a, q.slot[id(bn)]) if (need8 and a is not None) else None
         if not fused3:
+            q8 = q.out_for(a, q.slot[id(bn)]) if need8 else None
             # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue (1/16
             # of the bytes of re-reading the output there)
             ym = torch.empty(a.numel() // 8, device=a.device, dtype=torch.uint8) if fuse_next else None

@@ -141,7 +141,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
               tile: int = 0, stem: bool = False, epi: int = 0,
               fp8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, affine: Optional[torch.Tensor] = None,
               accumulate: bool = False, xbn: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None,
-              maskout: Optional[torch.Tensor] = None, res_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+              maskout: Optional[torch.Tensor] = None, res_scale: Optional[torch.Tensor] = None,
+              q8out=None) -> torch.Tensor:
     """y[N,OH,OW,Co] = conv(x[N,H,W,Ci], w[Co,KH,KW,Ci]) (+bias) (ReLU); optional
     per-channel (sum, sumsq) accumulation into ``stats`` (a [STAT_SLOTS, 2, Co]
     slab), or, given a BatchNorm workspace (``bn.work``), into its slab as
@@ -161,7 +162,8 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
     ``res`` (like ``out``): added after ``affine`` and before ``relu`` (training: a block's last BatchNorm +
     shortcut + ReLU in the conv's epilogue); ``maskout`` (uint8, numel / 8): also the ReLU mask of the stored
     output as bits; ``res_scale`` (fp32 [Co]): the residual enters as res * res_scale (a downsample block's
-    shortcut BatchNorm, its shift folded into ``affine``). All three: the streaming 1x1 kernel only."""
+    shortcut BatchNorm, its shift folded into ``affine``); ``q8out`` = (y8 uint8 like ``out``, exponent int32[1],
+    amax fp32[32]): also the delayed-scaled e4m3 copy of the output. All four: the streaming 1x1 kernel only."""
     N, H, W, Ci = x.shape
     Co = w.shape[0]
     OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
@@ -188,6 +190,11 @@ def igemm_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, KH: int, 
         if res_scale is not None:
             assert res_scale.dtype == torch.float32 and res_scale.numel() == Co and res_scale.is_contiguous()
             a.bnsave2 = res_scale.data_ptr()
+    if q8out is not None:
+        y8, e8, a8 = q8out
+        assert y8.dtype == torch.uint8 and y8.numel() == out.numel() and e8.dtype == torch.int32
+        a.flags |= 32768
+        a.Y8, a.y8exp, a.y8amax = y8.data_ptr(), e8.data_ptr(), a8.data_ptr()
     if maskout is not None:
         assert maskout.dtype == torch.uint8 and maskout.numel() * 8 == out.numel() and relu
         a.flags |= 16384

@@ -2,7 +2,10 @@
 hardware queue each stream's kernels ran on, busy time per stream per step,
 and how much of the weight-gradient stream's time overlapped the main stream.
 
-    python scripts/stream_timeline.py gpurun_out/prof/run_results.db [--marker sgd_kernel] [--skip 3]
+    python scripts/stream_timeline.py gpurun_out/prof/run_results.db [--marker sgd_kernel] [--skip 3] [--kernels 30]
+
+``--kernels N``: also a per-stream kernel table (the N largest kernels of each stream by in-step time), so the
+main stream's critical-path ranking is not mixed with the side-stream weight gradients.
 """
 import argparse
 import collections
@@ -33,6 +36,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--marker", default="sgd_kernel")
     ap.add_argument("--skip", type=int, default=3)
+    ap.add_argument("--kernels", type=int, default=0)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, stream_id, queue_id from kernels order by start").fetchall()
@@ -43,7 +47,11 @@ def main():
     by = collections.defaultdict(list)
     sq = collections.defaultdict(set)
     names = collections.defaultdict(collections.Counter)
+    per = collections.defaultdict(lambda: collections.defaultdict(lambda: [0, 0]))
     for n, s, e, st, q in rows:
+        k = per[st][n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:100]]
+        k[0] += e - s
+        k[1] += 1
         by[st].append((s, e))
         sq[st].add(q)
         names[st][n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]] += 1
@@ -57,6 +65,12 @@ def main():
               f"{union(iv) / nsteps / 1e6:.2f} ms/step, overlapped with main {ov:.2f} ms/step | {top}")
     allv = [x for v in by.values() for x in v]
     print(f"GPU busy (any stream) {union(allv) / nsteps / 1e6:.2f} ms/step")
+    if a.kernels:
+        for st, iv in sorted(by.items(), key=lambda kv: -len(kv[1])):
+            tot = sum(v[0] for v in per[st].values()) / nsteps / 1e6
+            print(f"\nstream {st}: kernel sum {tot:.2f} ms/step\n\n| ms/step | calls/step | avg us | kernel |\n|---:|---:|---:|---|")
+            for k, (t, cnt) in sorted(per[st].items(), key=lambda kv: -kv[1][0])[: a.kernels]:
+                print(f"| {t / nsteps / 1e6:.3f} | {cnt // nsteps} | {t / cnt / 1e3:.1f} | `{k}` |")
 
 
 if __name__ == "__main__":

@@ -168,8 +168,9 @@ def _fq(t, e):
     return (t * 2.0 ** -e).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** e
 
 
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_fp8_forward_training_step(arch, monkeypatch):
+@pytest.mark.parametrize("arch,gram", [("resnet18", False), ("resnet50", False), ("resnet50", True)],
+                         ids=["resnet18", "resnet50", "resnet50-gram"])
+def test_fp8_forward_training_step(arch, gram, monkeypatch):
     """--dtype fp8: e4m3 forward convs where the 1-byte loop wins (ops.block.fp8_fwd_ok), e5m2 x e4m3 dgrads
     where fp8_dgrad_ok, bf16 elsewhere.
 
@@ -180,10 +181,17 @@ def test_fp8_forward_training_step(arch, monkeypatch):
     operands must be the fake-quantised bf16 activation / fp32 master weight
     with the tensor's current power-of-two scale, and its output must be the
     fp32 conv of those operands (up to the bf16 output rounding). End to end:
-    logits near the fp32 oracle, finite gradients, sane delayed scales."""
+    logits near the fp32 oracle, finite gradients, sane delayed scales. ``gram``: every bottleneck in the Gram
+    form (the row threshold off), so the block outputs whose e4m3 copies the next conv1 reads come out of conv3's
+    fused bn3 + shortcut + ReLU epilogue (IG_Q8OUT) -- checked exactly as the BN-pass copies."""
     import math
 
     import imagent_amd.ops.block as blk
+    if gram:
+        monkeypatch.setattr(blk, "_GRAM_MIN_ROWS", 0)
+        fused = []
+        real_f = blk.gram_fwd_stats
+        monkeypatch.setattr(blk, "gram_fwd_stats", lambda *a, **k: fused.append(1) or real_f(*a, **k))
     from imagent_amd.models import resnet
     from imagent_amd.models.native import bind_native
     checked = []
@@ -227,6 +235,8 @@ def test_fp8_forward_training_step(arch, monkeypatch):
     # input channels; ResNet-50 also its 1x1 convs with >= 512, or 256 into <= 128, input channels)
     want = [c for c in model.convs() if c is not model.conv1 and blk.fp8_fwd_ok(c)]
     assert want and len(checked) == len(want), (len(checked), len(want))
+    if gram:
+        assert len(fused) == 13, len(fused)
     l32 = ref(x[..., :3].float().permute(0, 3, 1, 2).contiguous())
     e_log = rel(logits, l32)
     print(f"fp8 {arch}: logits rel err vs fp32 {e_log:.3f}")
