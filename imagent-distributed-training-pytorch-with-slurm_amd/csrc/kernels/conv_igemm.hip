@@ -127,7 +127,16 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
         return conv_stream(a, st);
     }
-    if (a.X2) {  // two K segments (bn_gram.hip): the v3 loop only
+    if (a.X2) {  // two K segments (bn_gram.hip): the streaming kernel for 256 + 64 -> 64, else the v3 loop
+        // IMAGENT_GRAM_STREAM=0: the v3 loop for every shape (A/B)
+        static const bool gstream = [] {
+            const char* e = getenv("IMAGENT_GRAM_STREAM");
+            return !e || atoi(e) != 0;
+        }();
+        if (tile == 0 && gstream) {
+            const int r = conv_stream(a, st);
+            if (r != 1) return r;
+        }
         if (!v3_ok(a) || a.Nout % 64) return -106;
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
         if (a.Nout >= 512 && t8 >= 192) return launch_v3<256, 256, 2, 2, 8, 128>(a, st);

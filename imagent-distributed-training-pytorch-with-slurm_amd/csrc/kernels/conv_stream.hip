@@ -44,12 +44,21 @@ namespace {
 // 8-B loads (each predicated on the image border).
 // XBN: the pixel operand is relu(x * scale[c] + shift[c]) (a.xbn [2][C]), applied to each B fragment
 // in registers right before its MFMAs (8 channels per lane per k-step: 2 KS x 8 constants per lane)
-template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false>
+// K2: a second K segment of K2 channels from X2 (same pixels, row pitch K2; the weights' columns [K, K + K2)),
+// with IG_BNBWD the Gram-form conv3 dgrad over [g | h2] (bn_gram.hip): `bias` [Nout] is added to the sums
+// before the ReLU mask (as the v3 loop's two-segment form)
+template <bool STEM, int KT>
+constexpr int stream_rp() {  // LDS weight row pitch in 16-B chunks: 16-chunk swizzle groups stay inside the row
+    return STEM ? 32 : (KT / 8 <= 16 ? KT / 8 : (KT / 8 + 15) / 16 * 16);
+}
+
+template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false, int K2 = 0>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) {
-    constexpr int KS = K / 32;        // MFMA k-steps per group
+    constexpr int KS1 = K / 32;       // k-steps from X
+    constexpr int KS = (K + K2) / 32; // MFMA k-steps per group
     constexpr int FN = BN / 16;       // channel fragments
-    constexpr int CPR = K / 8;        // 16-B chunks per weight row
-    constexpr int RP = STEM ? 32 : CPR;             // LDS weight row pitch, chunks (power of two)
+    constexpr int CPR = (K + K2) / 8; // 16-B chunks per weight row
+    constexpr int RP = stream_rp<STEM, K + K2>();   // LDS weight row pitch, chunks
     constexpr int RB = RP * 16;                     // ... bytes
     constexpr int SWM = (RP < 16 ? RP : 16) - 1;    // chunk swizzle mask: conflict-free A reads
     constexpr int EP = BN * 2 + 16;   // epilogue LDS row pitch (bytes)
@@ -136,6 +145,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     float s1[8], s2[8], s3[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) s1[c] = s2[c] = s3[c] = 0.f;
+    float gbias[K2 > 0 ? 8 : 1];
+    if constexpr (K2 > 0) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) gbias[c] = a.bias[n + c];
+    }
 
     const int ohw = a.OH * a.OW;
     const bool dense = a.sA == 1 && a.H == a.OH && a.W == a.OW;  // input row == output pixel
@@ -185,8 +199,14 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
         }
         const bf16_t* p = a.X + row * a.C + fq * 8;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
+        for (int ks = 0; ks < KS1; ++ks)
             pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(p + ks * 32) : u32x4{0u, 0u, 0u, 0u};
+        if constexpr (K2 > 0) {  // (dense rows only: host check)
+            const bf16_t* p2 = a.X2 + row * K2 + fq * 8;
+#pragma unroll
+            for (int ks = KS1; ks < KS; ++ks)
+                pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(p2 + (ks - KS1) * 32) : u32x4{0u, 0u, 0u, 0u};
+        }
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) fetch(d, w0 + d * wstride);
@@ -318,6 +338,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             v[2 * k + 1] = fmaxf(v[2 * k + 1], 0.f);
                         }
                     }
+                    if constexpr (K2 > 0) {
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) v[c] += gbias[c];
+                    }
                     float xv[8];
                     if (bnb) {
 #pragma unroll
@@ -415,17 +439,17 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     }
 }
 
-template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false>
+template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false, int K2 = 0>
 int launch_stream1(const IGemmArgs& a, hipStream_t st) {
-    constexpr int RP = STEM ? 32 : K / 8;
+    constexpr int RP = stream_rp<STEM, K + K2>();
     const size_t lds = (size_t)BN * RP * 16 + 4 * 16 * (BN * 2 + 16);
     static int resident = 0;
-    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM, XBN>, lds);
+    if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM, XBN, K2>, lds);
     const int nsl = a.Nout / BN;
     const int ngroups = (a.M + 15) / 16;
     // enough pixel blocks to fill the chip, but >= D groups per wave
     const int npb = std::max(1, std::min(resident / nsl, (ngroups + 4 * D - 1) / (4 * D)));
-    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM, XBN>), dim3(npb * nsl), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((conv_stream_kernel<K, BN, D, MODE, STEM, XBN, K2>), dim3(npb * nsl), dim3(256), lds, st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
@@ -462,6 +486,19 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
          ((a.flags & IG_Q8OUT) && (!a.Y8 || !a.y8exp || !a.y8amax))))
         return -121;
     const bool has_bias = a.bias && !eval_bn;
+    if (a.X2) {
+        // the Gram-form conv3 dgrad of a 64-channel bottleneck (bn_gram.hip): K = [g (256) | h2 (64)] into 64
+        // channels with bn2's BN-backward epilogue, weights [64][320] resident in LDS (the 128 x 64 v3 tile
+        // re-stages them per tile and ran these HBM streams at ~2.7 TB/s)
+        if (!(a.flags & IG_BNBWD) || (a.flags & (IG_ACCUM | IG_FP8 | IG_OUT_F32 | IG_AFFINE | IG_NOSTREAM | IG_RES |
+                                                  IG_MASKOUT | IG_Q8OUT)) ||
+            a.C != 256 || a.C2 != 64 || a.Nout != 64 || a.ldb != 320 || a.ldy != 64 || !a.bias || a.bnx2 ||
+            a.nth != 1 || a.ntw != 1 || a.sA != 1 || a.H != a.OH || a.W != a.OW || a.sY != 1 || a.YH != a.OH ||
+            a.YW != a.OW || a.dh0 != 0 || a.dw0 != 0 || a.kh0 != 0 || a.kw0 != 0 || a.oy != 0 || a.ox != 0)
+            return 1;
+        return a.bnym ? launch_stream1<256, 64, 2, 1, false, false, 64>(a, st)
+                      : launch_stream1<256, 64, 2, 2, false, false, 64>(a, st);
+    }
     if (a.flags & IG_STEM) {  // 7x7 stem, C = 4, K = 7 x 32
         if (a.flags & (IG_OUT_F32 | IG_FP8 | IG_ACCUM | IG_BNBWD | IG_NOSTREAM)) return 1;
         if (has_bias || a.C != 4 || a.nth != 7 || a.ntw > 8 || a.ldb != 7 * 32 || a.Nout % 64 || a.ldy != a.Nout ||
