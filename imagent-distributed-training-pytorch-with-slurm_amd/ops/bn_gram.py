@@ -16,11 +16,25 @@ in forward (``ops/block.py``)."""
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, streams
 from .conv import BNBwdFuse, _base_args, _igemm_call, colsum_into, igemm_wgrad
 from .grad_sink import notify_ready
+
+# split-K of the skinny Gram GEMMs (T = g^T h2, G = h2^T h2: a [4p][p] / [p][p] output over M ~ 1e5-3e6 pixels):
+# one wave of 512 blocks (2 per CU) on the v3 weight-gradient loop -- scripts/gram_bench.py at 1024 img, isolated:
+# G 128x128 90 -> 66 us, 256x256 74 -> 52, T 512x128 223 -> 187, 1024x256 186 -> 167 (the default 1024-block
+# target pays a second, partial wave). IMAGENT_GRAM_SPLITS=0: the default split (A/B).
+_GRAM_SPLITS = os.environ.get("IMAGENT_GRAM_SPLITS", "1") != "0"
+
+
+def _splits(co: int, ci: int) -> int:
+    if not _GRAM_SPLITS or co % 128 or ci % 128:  # (the register-staged kernel keeps its own choice)
+        return 0
+    return max(16, 512 // ((co // 128) * (ci // 128)))
 
 
 class GramBN:
@@ -37,7 +51,7 @@ def gram_T(g: torch.Tensor, h2: torch.Tensor, out: torch.Tensor = None) -> torch
     """T = g^T h2 [4p][p] fp32 (conv3's weight-gradient GEMM), on the current stream (``out``: zeroed)."""
     C4, p = g.shape[-1], h2.shape[-1]
     T = out if out is not None else torch.zeros((C4, p), device=g.device, dtype=torch.float32)
-    igemm_wgrad(g, h2, T, 1, 0, 1, 1)
+    igemm_wgrad(g, h2, T, 1, 0, 1, 1, splits=_splits(g.shape[-1], h2.shape[-1]))
     return T
 
 
@@ -99,7 +113,7 @@ def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor)
     / ``save``. Returns (aff [2][4p] = (gamma rstd, beta - mean gamma rstd) for conv3's epilogue, P; the weight
     gradient reuses G and P)."""
     C4, p = conv.out_channels, conv.in_channels
-    igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
+    igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
     P = torch.mm(conv.w_bf16.view(C4, p).float(), G)
     aff = torch.empty((2, C4), device=h2.device, dtype=torch.float32)
     w = bn.work
@@ -133,12 +147,12 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
         T = gb.T
         if T is None:  # (else formed on the main stream for the coefficients: g is not read here)
             T = torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
-            igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1)
+            igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1, splits=_splits(C4, p))
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record(side)
         if P is None:
-            igemm_wgrad(h2, h2, G, 1, 0, 1, 1)
+            igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
         if own_s:
             colsum_into(h2.view(-1, p), s)
         if P is None:

@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--variants", default="0,-1,1,2,3,4")
+    ap.add_argument("--splits", default="0", help="split-K counts to try (0: the kernel's own choice)")
     args = ap.parse_args()
     from imagent_amd.ops.conv import igemm_wgrad
     B = args.batch
@@ -42,6 +43,7 @@ def main():
         shapes.append((f"T  {4 * p}x{p} @{hw}", hw, 4 * p, p))
         shapes.append((f"G  {p}x{p} @{hw}", hw, p, p))
     variants = [int(v) for v in args.variants.split(",")]
+    splits = [int(v) for v in args.splits.split(",")]
     for label, hw, co, ci in shapes:
         M = B * hw * hw
         torch.manual_seed(0)
@@ -54,15 +56,17 @@ def main():
         t = timeit(lambda: torch.mm(dy.view(M, co).t(), x.view(M, ci)))
         line += f" mm {t:7.1f} us {gb / t * 1e3:5.2f} TB/s |"
         for v in variants:
-            try:
-                out.zero_()
-                igemm_wgrad(dy, x, out, 1, 0, 1, 1, variant=v)
-                torch.cuda.synchronize()
-                err = (out - ref).norm().item() / ref.norm().item()
-                t = timeit(lambda: igemm_wgrad(dy, x, out, 1, 0, 1, 1, variant=v))
-                line += f" v{v} {t:7.1f} us {gb / t * 1e3:5.2f} TB/s e{err:.0e} |"
-            except Exception as ex:  # shape not covered by this variant
-                line += f" v{v} n/a |"
+            for sp in splits:
+                tag = f"v{v}" + (f"/s{sp}" if sp else "")
+                try:
+                    out.zero_()
+                    igemm_wgrad(dy, x, out, 1, 0, 1, 1, splits=sp, variant=v)
+                    torch.cuda.synchronize()
+                    err = (out - ref).norm().item() / ref.norm().item()
+                    t = timeit(lambda: igemm_wgrad(dy, x, out, 1, 0, 1, 1, splits=sp, variant=v))
+                    line += f" {tag} {t:6.1f} us {gb / t * 1e3:4.2f} TB/s e{err:.0e} |"
+                except Exception:  # shape not covered by this variant
+                    line += f" {tag} n/a |"
         print(line, flush=True)
 
 
