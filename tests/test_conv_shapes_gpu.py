@@ -11,7 +11,7 @@ the kernel names the auto-dispatch launched are recorded with torch.profiler
 (``gpurun_out/conv_shape_kernels.json``, committed as
 ``profiles/conv_shape_kernels.md``); the set over all shapes must cover the
 conv kernels of the bench's rocprof trace (``BENCH_KERNELS``, from
-``profiles/r50_b1024_v18_kernel_stats.md``).
+``profiles/r50_b1024_v21_stream_tables.md``).
 Reference ops: torchvision resnet convs (imagenet.py:312, fwd :123, bwd :128).
 """
 
@@ -39,26 +39,23 @@ def _shapes(arch, size, batch):
 
 SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _shapes("resnet18", 448, 128)
 
-# conv kernel templates in the R50 bench trace (round 4, profiles/r50_b1024_v18_kernel_stats.md: v3 with its
-# element-size / format template arguments, K = 256 fused BN-backward dgrads on the streaming kernel); update
-# together with the dispatcher. Not listed: igemm_v3_kernel<128, 64, 1, 2, 4, 128, 2, 0>, the Gram-form bn3 dgrad
-# of the 64-channel stage (two K segments, no plain conv shape takes it; tests/test_model_gpu.py
-# test_bn_gram_backward_matches_torch covers it against the fp32 model).
+# conv kernel templates in the R50 bench trace (round 4 HEAD, profiles/r50_b1024_v21_stream_tables.md: v3 with its
+# element-size / format template arguments, the streaming kernel with its second-K-segment width); update together
+# with the dispatcher. Not listed (no plain conv shape takes them; tests/test_model_gpu.py covers them against the
+# fp32 model in test_bn_gram_backward_matches_torch and test_fp8_forward_training_step[resnet50-gram]): the
+# fused-output conv3 mode conv_stream_kernel<*, *, *, 4, ...> (bn3 + shortcut + ReLU + mask bits / e4m3 copy) and
+# the Gram-form bn3 dgrad over [g | h2], conv_stream_kernel<256, 64, 2, 2, false, false, 64>.
 BENCH_KERNELS = [
-    "conv_stream_kernel<128, 128, 2, 0, false, false>",
-    "conv_stream_kernel<128, 128, 2, 0, false, true>",
-    "conv_stream_kernel<128, 128, 2, 1, false, false>",
-    "conv_stream_kernel<128, 128, 2, 3, false, false>",
-    "conv_stream_kernel<224, 64, 2, 0, true, false>",
-    "conv_stream_kernel<256, 64, 2, 0, false, false>",
-    "conv_stream_kernel<256, 64, 2, 1, false, false>",
-    "conv_stream_kernel<256, 64, 2, 2, false, false>",
-    "conv_stream_kernel<256, 64, 2, 3, false, false>",
-    "conv_stream_kernel<64, 128, 3, 1, false, false>",
-    "conv_stream_kernel<64, 128, 3, 3, false, false>",
-    "conv_stream_kernel<64, 256, 3, 0, false, false>",
-    "conv_stream_kernel<64, 256, 3, 0, false, true>",
-    "conv_stream_kernel<64, 64, 3, 0, false, false>",
+    "conv_stream_kernel<128, 128, 2, 1, false, false, 0>",
+    "conv_stream_kernel<128, 128, 2, 3, false, false, 0>",
+    "conv_stream_kernel<224, 64, 2, 0, true, false, 0>",
+    "conv_stream_kernel<256, 64, 2, 0, false, false, 0>",
+    "conv_stream_kernel<256, 64, 2, 1, false, false, 0>",
+    "conv_stream_kernel<256, 64, 2, 3, false, false, 0>",
+    "conv_stream_kernel<64, 128, 3, 1, false, false, 0>",
+    "conv_stream_kernel<64, 128, 3, 3, false, false, 0>",
+    "conv_stream_kernel<64, 256, 3, 0, false, false, 0>",
+    "conv_stream_kernel<64, 64, 3, 0, false, false, 0>",
     "halo3x3_kernel<56, 4, 0>",
     "halo3x3_kernel<56, 4, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0, 128>",
@@ -69,7 +66,6 @@ BENCH_KERNELS = [
     "wgrad_halo_kernel<28, 4, 4, 32, 1>",
     "wgrad_halo_kernel<56, 4, 7, 64, 1>",
     "wgrad_kernel<128, 128, 2, false, 4, 32, false>",
-    "wgrad_kernel<128, 128, 2, false, 4, 32, true>",
     "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
     "wgrad_kernel<64, 128, 1, true, 4, 32, false>",
