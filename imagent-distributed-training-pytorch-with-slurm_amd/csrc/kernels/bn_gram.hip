@@ -75,6 +75,32 @@ __global__ __launch_bounds__(256) void bn_gram_dgrad_weights_kernel(const bf16_t
     if (threadIdx.x == 0) bias[i] = red[0];
 }
 
+// Q = W3^T diag(B) W3 [p][p] for the folded dgrad weights: Q[i][j] = sum_o wt[i][o] B[o] wt[j][o] (wt = W3^T,
+// [p][ldw] bf16, B = coef[C4 ..]). One 16 x 16 output tile per block, the two row bands staged through LDS in
+// 64-wide K chunks: (p / 16)^2 blocks. (torch.mm ran the p = 128 case as ONE 128 x 128 hipBLASLt workgroup:
+// 36 us alone, 200-360 us in the step next to the weight-gradient stream.)
+__global__ __launch_bounds__(256) void bn_gram_q_kernel(const bf16_t* __restrict__ wt, int ldw,
+                                                        const float* __restrict__ coef, float* __restrict__ Q, int p,
+                                                        int C4) {
+    __shared__ float sa[16][65], sb[16][65];
+    const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+    const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+    float acc = 0.f;
+    for (int k0 = 0; k0 < C4; k0 += 64) {
+        for (int e = threadIdx.x; e < 16 * 64; e += 256) {
+            const int r = e >> 6, k = e & 63, o = k0 + k;
+            const bool ok = o < C4;
+            sa[r][k] = ok ? bf2f(wt[(size_t)(i0 + r) * ldw + o]) * coef[C4 + o] : 0.f;
+            sb[r][k] = ok ? bf2f(wt[(size_t)(j0 + r) * ldw + o]) : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) acc = fmaf(sa[ti][k], sb[tj][k], acc);
+        __syncthreads();
+    }
+    Q[(size_t)(i0 + ti) * p + j0 + tj] = acc;
+}
+
 // dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + c_o s[i]   (T = g^T h2, P = W3 G, s = colsum h2)
 __global__ __launch_bounds__(256) void bn_gram_wgrad_fixup_kernel(float* __restrict__ dw,
                                                                   const float* __restrict__ T,
@@ -180,6 +206,14 @@ IMK_EXPORT int imk_bn_gram_dgrad_weights(const void* wt, int ldw, const float* c
     if (p <= 0 || C4 <= 0 || ldw < C4) return -100;
     hipLaunchKernelGGL(bn_gram_dgrad_weights_kernel, dim3(p), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)wt, ldw, coef, Q, (bf16_t*)wcat, bias, p, C4);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_gram_q(const void* wt, int ldw, const float* coef, float* Q, int p, int C4, void* stream) {
+    if (p <= 0 || p % 16 || C4 <= 0 || ldw < C4) return -100;
+    hipLaunchKernelGGL(bn_gram_q_kernel, dim3(p / 16, p / 16), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)wt,
+                       ldw, coef, Q, p, C4);
     IMK_CHECK_LAUNCH();
     return 0;
 }

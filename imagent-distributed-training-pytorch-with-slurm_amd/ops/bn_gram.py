@@ -86,12 +86,19 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     p = h2.shape[-1]
     wt = conv.wt_bf16  # [p][1][1][4p] = W3^T
     assert tuple(wt.shape) == (p, 1, 1, C4) and conv.kh == 1 and conv.stride == 1
-    Wf = wt.view(p, C4).float()
-    Q = torch.mm(Wf * gb.coef[1], Wf.t())  # W3^T diag(B) W3 [p][p] (symmetric)
     wcat = torch.empty((p, C4 + p), device=h2.device, dtype=torch.bfloat16)
     bias = torch.empty((p,), device=h2.device, dtype=torch.float32)
     k = _lib.kernels()
     st = _lib.stream_ptr()
+    # Q = W3^T diag(B) W3 [p][p] (symmetric). hipBLASLt runs p = 128 as ONE 128 x 128 workgroup (36 us alone,
+    # 200-360 us in the step beside the weight-gradient stream): the own 16 x 16-tile kernel there (32 us in the
+    # step); p = 64 / 256 keep torch.mm (12-18 us in the step vs 15-23 / 54 us)
+    if p == 128:
+        Q = torch.empty((p, p), device=h2.device, dtype=torch.float32)
+        _lib.check(k.imk_bn_gram_q(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), p, C4, st), "gram Q")
+    else:
+        Wf = wt.view(p, C4).float()
+        Q = torch.mm(Wf * gb.coef[1], Wf.t())
     _lib.check(k.imk_bn_gram_dgrad_weights(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), wcat.data_ptr(),
                                            bias.data_ptr(), p, C4, st), "gram dgrad weights")
     out = torch.empty((N, H, W, p), device=h2.device, dtype=torch.bfloat16)
