@@ -64,6 +64,13 @@ struct Comm {
     // calls currently inside RCCL with this communicator (InFlight guards); imc_abort waits for it to
     // drain (bounded) before ncclCommAbort frees the communicator
     std::atomic<int> inflight{0};
+    // who tears the communicator down, decided once (compare-exchange from 0): 1 = imc_abort (the watchdog),
+    // 2 = imc_comm_destroy. The loser never touches the handle: a destroy that loses waits for `torn`, an abort
+    // that loses returns (destroy's settle() sees `aborting` and aborts instead of finalising). The Comm object
+    // itself is never freed (a few hundred bytes per communicator), so a watchdog that fires after destroy
+    // returned reads valid memory and leaves.
+    std::atomic<int> owner{0};
+    std::atomic<bool> torn{false};  // the owner is done with the handle (last store of the owner)
     hipStream_t stream = nullptr;
     int rank = 0, nranks = 1, device = 0, n_events = 64, stream_mode = 0;
     std::vector<hipEvent_t> events;   // ring of reusable events
@@ -300,15 +307,29 @@ int32_t imc_comm_nranks(void* h) {
 int32_t imc_comm_destroy(void* h) {
     Comm* c = static_cast<Comm*>(h);
     if (!c) return 0;
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm && !c->aborting.load(std::memory_order_seq_cst)) {
-        // a non-blocking communicator finalises asynchronously
-        if (settle(c, ncclCommFinalize(c->comm)) == ncclSuccess) ncclCommDestroy(c->comm);
-        else ncclCommAbort(c->comm);
+    int expect = 0;
+    if (c->owner.compare_exchange_strong(expect, 2, std::memory_order_seq_cst)) {
+        if (c->stream && !c->aborting.load(std::memory_order_seq_cst)) (void)hipStreamSynchronize(c->stream);
+        if (c->comm) {
+            // a non-blocking communicator finalises asynchronously; settle() leaves early once a concurrent
+            // imc_abort raised `aborting` (that abort lost the ownership race and does not touch the handle)
+            if (!c->aborting.load(std::memory_order_seq_cst) && settle(c, ncclCommFinalize(c->comm)) == ncclSuccess)
+                ncclCommDestroy(c->comm);
+            else
+                ncclCommAbort(c->comm);
+        }
+        c->torn.store(true, std::memory_order_seq_cst);
+    } else if (expect == 1) {
+        // the watchdog's abort owns the teardown: wait for it (bounded by its drain + ncclCommAbort)
+        while (!c->torn.load(std::memory_order_seq_cst)) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    } else {
+        return 0;  // destroyed before
     }
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->events) (void)hipEventDestroy(e);
+    c->events.clear();
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    delete c;
+    c->stream = nullptr;
     return 0;
 }
 
@@ -424,13 +445,22 @@ constexpr double ABORT_DRAIN_S = 5.0;
 
 int32_t imc_abort(void* h) {
     Comm* c = static_cast<Comm*>(h);
-    if (c && !c->aborting.exchange(true, std::memory_order_seq_cst) && c->comm) {
+    if (!c) return 0;
+    c->aborting.store(true, std::memory_order_seq_cst);
+    int expect = 0;
+    if (!c->owner.compare_exchange_strong(expect, 1, std::memory_order_seq_cst)) return 0;  // destroy / abort ran
+    if (c->comm) {
         const auto t0 = std::chrono::steady_clock::now();
         while (c->inflight.load(std::memory_order_seq_cst) > 0 &&
                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < ABORT_DRAIN_S)
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        const int left = c->inflight.load(std::memory_order_seq_cst);
+        if (left > 0)
+            fprintf(stderr, "[imagent rccl] abort: drain timed out after %.0f s with %d call(s) still inside RCCL\n",
+                    ABORT_DRAIN_S, left);
         ncclCommAbort(c->comm);
     }
+    c->torn.store(true, std::memory_order_seq_cst);
     return 0;
 }
 

@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ scratch, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
     const bf16_t* __restrict__ x2, const float* __restrict__ save2, const float* __restrict__ gamma2,
     bf16_t* __restrict__ dx2, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8) {
+    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8, int sgxo) {
     constexpr int UB = MODE == 2 ? 2 : U;  // three streams in, two out: half the rows in flight
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
     const float qs0 = Q8 && g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     float m0 = 0.f, m1 = 0.f;
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
-            if (dgamma) dgamma[c] += scratch[c];
+            if (dgamma) dgamma[c] += scratch[sgxo + c];
             if (dbeta) dbeta[c] += scratch[C + c];
             if (MODE == 2) {
                 if (dgamma2) dgamma2[c] += scratch[2 * C + c];
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             sh[i] = beta[c] - mean * gr;
         }
         k1[i] = gr;
-        kx[i] = -gr * inv_cnt * scratch[c] * rstd;
+        kx[i] = -gr * inv_cnt * scratch[sgxo + c] * rstd;
         k0[i] = -gr * inv_cnt * scratch[C + c] - kx[i] * mean;
         if (MODE == 2) {
             const float m2 = save2[c], rs2 = save2[C + c];
@@ -637,15 +637,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
 }
 
-// non-temporal stores of the streamed outputs (IMAGENT_BN_NT=0 turns them off): scripts/bn_bench.py at
-// batch 1024, per step fwd 9328 -> 9077 us, bwd apply 12310 -> 12053 us
-bool bn_nt() {
-    static const bool v = [] {
-        const char* e = getenv("IMAGENT_BN_NT");
-        return !e || atoi(e) != 0;
-    }();
-    return v;
-}
+// non-temporal stores of the streamed outputs: scripts/bn_bench.py at batch 1024, per step fwd 9328 -> 9077 us,
+// bwd apply 12310 -> 12053 us (round 3; in-step within noise at round-4 HEAD, kept)
+constexpr bool bn_nt() { return true; }
 
 // Streaming passes size their grid by grid_for (<= 2048 blocks = 8 per CU); a variant whose registers allow
 // fewer resident blocks per CU (bn_fwd mode 1: 94 VGPRs, 5 waves / SIMD) then runs its grid-stride loop in
@@ -742,8 +736,11 @@ IMK_EXPORT int imk_bn_affdesc_size() { return (int)sizeof(AffDesc); }
 IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save, const float* gamma,
                                 const void* x2, const float* save2, const float* gamma2, float* scratch,
                                 void* dx, void* dx2, float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
-                                float* dbeta2_acc, long R, int C, int mode, const void* g8desc, void* stream) {
-    if (C % 8 || C > 2048) return -100;
+                                float* dbeta2_acc, long R, int C, int mode, const void* g8desc, int sgx_row,
+                                void* stream) {
+    // sgx_row (mode 0 / 1): the slab row holding sum(g xhat) -- 2 when `scratch` is a Gram-form bn3's slab whose
+    // third row the producing dgrad filled with the downsample BN's sum(g xhat_d) (ops/block.py)
+    if (C % 8 || C > 2048 || sgx_row < 0 || sgx_row > 2 || (mode == 2 && sgx_row)) return -100;
     // g8desc (host pointer, may be null): {q0, q1, exp0, exp1, amax0, amax1} device pointers of the
     // e5m2 copies of dx / dx2 (fp8 dgrad)
     G8Out g8{};
@@ -770,7 +767,7 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
                        dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
                        nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr,       \
                        (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,               \
-                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8)
+                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8, sgx_row * C)
 #define LA(M)                                                                  \
     do {                                                                       \
         if (q8) { if (nt) LK(M, true, true); else LK(M, false, true); }        \
@@ -868,7 +865,7 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M, false, false>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
                        (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, folded, (bf16_t*)dx,   \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
-                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{})
+                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{}, 0)
     if (mode == 0) { if (relu == 2) LA(2, 0); else if (relu) LA(1, 0); else LA(0, 0); }
     else if (mode == 1) { if (relu) LA(1, 1); else LA(0, 1); }
     else { if (relu) LA(1, 2); else LA(0, 2); }

@@ -75,63 +75,107 @@ __global__ __launch_bounds__(256) void bn_gram_dgrad_weights_kernel(const bf16_t
     if (threadIdx.x == 0) bias[i] = red[0];
 }
 
-// Q = W3^T diag(B) W3 [p][p] for the folded dgrad weights: Q[i][j] = sum_o wt[i][o] B[o] wt[j][o] (wt = W3^T,
-// [p][ldw] bf16, B = coef[C4 ..]). One 16 x 16 output tile per block, the two row bands staged through LDS in
-// 64-wide K chunks: (p / 16)^2 blocks. (torch.mm ran the p = 128 case as ONE 128 x 128 hipBLASLt workgroup:
-// 36 us alone, 200-360 us in the step next to the weight-gradient stream.)
-__global__ __launch_bounds__(256) void bn_gram_q_kernel(const bf16_t* __restrict__ wt, int ldw,
-                                                        const float* __restrict__ coef, float* __restrict__ Q, int p,
-                                                        int C4) {
-    __shared__ float sa[16][65], sb[16][65];
-    const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
-    const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
-    float acc = 0.f;
-    for (int k0 = 0; k0 < C4; k0 += 64) {
-        for (int e = threadIdx.x; e < 16 * 64; e += 256) {
-            const int r = e >> 6, k = e & 63, o = k0 + k;
-            const bool ok = o < C4;
-            sa[r][k] = ok ? bf2f(wt[(size_t)(i0 + r) * ldw + o]) * coef[C4 + o] : 0.f;
-            sb[r][k] = ok ? bf2f(wt[(size_t)(j0 + r) * ldw + o]) : 0.f;
+// The small fp32 GEMMs of the Gram form, C[M][N] = sum_k A(m, k) B(k, n), on the VALU (fp32 products: P feeds
+// bn3's variance, which must not lose what the centring keeps). 64 x 64 output tile per block, 4 x 4 per thread,
+// K staged through LDS in chunks of 16 ([k][m] / [k][n] images read as float4). No split-K, no atomics: the
+// grids are small (16 - 64 blocks at R50) and run beside the weight-gradient stream. M, N % 64 == 0, K % 16 == 0.
+//  MODE 0: P = W3 Gc, the centred Gram matrix Gc = G - s s^T / rows formed on the operand load
+//          (A(o, j) = W3[o][j], bf16 [C4][p]; B(j, i) = G[j][i] - s[j] s[i] / rows; M = C4, N = K = p);
+//  MODE 1: Q = W3^T diag(B) W3 for the folded dgrad weights (A(i, o) = wt[i][o] B_o, B(o, j) = wt[j][o],
+//          wt = W3^T [p][ldw] bf16, B = coef[C4 ..]; M = N = p, K = C4).
+// (torch.mm ran these as 16-workgroup hipBLASLt kernels plus bf16 -> fp32 weight casts: 160 us per P call in
+// the step, profiles/r50_b1024_v21_stream_tables.md)
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_gram_gemm_kernel(const bf16_t* __restrict__ w, int ldw,
+                                                           const float* __restrict__ G, const float* __restrict__ s,
+                                                           const float* __restrict__ coef, float* __restrict__ out,
+                                                           int M, int N, int K, float inv_rows) {
+    __shared__ __attribute__((aligned(16))) float sa[16][68], sb[16][68];
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // A: 64 rows x 16 k, k fastest in memory
+            const int e = tid + 256 * q, r = e >> 4, kk = e & 15;
+            float v = bf2f(w[(size_t)(m0 + r) * ldw + k0 + kk]);
+            if (MODE == 1) v *= coef[K + k0 + kk];
+            sa[kk][r] = v;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            if (MODE == 0) {  // B: 16 k x 64 n, n fastest in memory
+                const int kk = e >> 6, c = e & 63;
+                const int j = k0 + kk, i = n0 + c;
+                sb[kk][c] = G[(size_t)j * N + i] - s[j] * s[i] * inv_rows;
+            } else {  // B(o, j) = wt[j][o]: k fastest in memory
+                const int c = e >> 4, kk = e & 15;
+                sb[kk][c] = bf2f(w[(size_t)(n0 + c) * ldw + k0 + kk]);
+            }
         }
         __syncthreads();
-#pragma unroll 16
-        for (int k = 0; k < 64; ++k) acc = fmaf(sa[ti][k], sb[tj][k], acc);
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const f32x4 a4 = *reinterpret_cast<const f32x4*>(&sa[kk][ty * 4]);
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sb[kk][tx * 4]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a4[i], b4[j], acc[i][j]);
+        }
         __syncthreads();
     }
-    Q[(size_t)(i0 + ti) * p + j0 + tj] = acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<f32x4*>(out + (size_t)(m0 + ty * 4 + i) * N + n0 + tx * 4) =
+            f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
 }
 
-// dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + c_o s[i]   (T = g^T h2, P = W3 G, s = colsum h2)
+// dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + (c_o + B_o mean_o) s[i]   (T = g^T h2, P = W3 Gc with the centred
+// Gram matrix, s = colsum h2). From dW3 = dx3^T h2 = A T + B W3 G + c s^T and W3 G = P + mean s^T: the centred form
+// adds no two large, nearly equal terms when |mean| >> std (c_o + B_o mean_o = -A_o mean(g) is small)
 __global__ __launch_bounds__(256) void bn_gram_wgrad_fixup_kernel(float* __restrict__ dw,
                                                                   const float* __restrict__ T,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ coef,
+                                                                  const float* __restrict__ mean,
                                                                   const float* __restrict__ s, int C4, int p) {
     const long n = (long)C4 * p;
     for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
         const int o = (int)(e / p), i = (int)(e - (long)o * p);
-        dw[e] += fmaf(coef[o], T[e], fmaf(coef[C4 + o], P[e], coef[2 * C4 + o] * s[i]));
+        const float k0 = fmaf(coef[C4 + o], mean[o], coef[2 * C4 + o]);
+        dw[e] += fmaf(coef[o], T[e], fmaf(coef[C4 + o], P[e], k0 * s[i]));
     }
 }
 
 // As bn_bwd_coef_kernel, with sum(g xhat) NOT from the slab but from T = g^T h2 (the weight gradient's GEMM):
-// x3 = h2 W3^T, so sum_m g[m][o] x3[m][o] = sum_i W3[o][i] T[o][i] and sum(g xhat) = rstd (that - mean sum(g)).
-// The producing dgrad then never reads x3 (BNBwdFuse without x). One wave per channel.
+// x3 = h2 W3^T, so sum_m g[m][o] (x3[m][o] - mean_o) = sum_i W3[o][i] (T[o][i] - sg_o mu_i), mu = colsum(h2) / rows,
+// centred per element (the uncentred rstd (W3 . T - mean sg) differences two large, nearly equal sums when
+// |mean| >> std). The producing dgrad then never reads x3 (BNBwdFuse without x). One wave per channel.
 __global__ __launch_bounds__(256) void bn_bwd_coef_T_kernel(const float* __restrict__ slab, const float* __restrict__ T,
-                                                            const bf16_t* __restrict__ w, const float* __restrict__ save,
+                                                            const bf16_t* __restrict__ w, const float* __restrict__ hs,
+                                                            const float* __restrict__ save,
                                                             const float* __restrict__ gamma, float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, float* __restrict__ coef, int S,
                                                             int C, int p, float inv_cnt) {
     const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (o >= C) return;  // wave-uniform
-    float dot = 0.f, sg = 0.f;
-    for (int i = lane; i < p; i += 64) dot += bf2f(w[(size_t)o * p + i]) * T[(size_t)o * p + i];
+    float sg = 0.f;
     for (int s = lane; s < S; s += 64) sg += slab[(size_t)s * 3 * C + C + o];
-    dot = wave_sum(dot);
     sg = wave_sum(sg);
+    const float sgm = sg * inv_cnt;
+    float dot = 0.f;
+    for (int i = lane; i < p; i += 64)
+        dot += bf2f(w[(size_t)o * p + i]) * fmaf(-sgm, hs[i], T[(size_t)o * p + i]);
+    dot = wave_sum(dot);
     if (lane) return;
     const float mean = save[o], rstd = save[C + o], gr = gamma[o] * rstd;
-    const float sgx = rstd * (dot - mean * sg);
+    const float sgx = rstd * dot;
     if (dgamma) dgamma[o] += sgx;
     if (dbeta) dbeta[o] += sg;
     const float k0 = -gr * inv_cnt * sg, kx = -gr * inv_cnt * sgx * rstd;
@@ -141,15 +185,18 @@ __global__ __launch_bounds__(256) void bn_bwd_coef_T_kernel(const float* __restr
 }
 
 // bn3's training statistics WITHOUT conv3's output (x3 = h2 W3^T, never written): per output channel o,
-//   mean = W3[o] . colsum(h2) / M,   E[x3^2] = W3[o] . (W3 G)[o] / M  (G = h2^T h2, P = W3 G),
-// var = E[x3^2] - mean^2 (biased, as the training BatchNorm normalises), -> stats [2][C] (mean, var; the running-
-// statistics update reads it), save [2][C] (mean, rstd; the backward), aff [2][C] (gamma rstd, beta - mean gamma
-// rstd; conv3's epilogue applies it). One wave per channel.
+//   mean = W3[o] . colsum(h2) / M,   var = W3[o] . P[o] / M  with P = W3 Gc, Gc = G - s s^T / M (G = h2^T h2),
+// i.e. var = W3[o]^T Cov(h2) W3[o]: the covariance is formed BEFORE the contraction with W3, so a channel whose
+// |mean| >> std (W3[o] aligned with the mean of h2) does not lose its variance to E[x3^2] - mean^2 cancellation
+// (tests/test_bn_numerics_gpu.py, |mean| / std >= 30 against fp64). Biased, as the training BatchNorm normalises.
+// -> stats [2][C] (mean, var; the running-statistics update reads it), save [2][C] (mean, rstd; the backward),
+// aff [2][C] (gamma rstd, beta - mean gamma rstd; conv3's epilogue applies it). One wave per channel.
 __global__ __launch_bounds__(256) void bn_gram_fwd_stats_kernel(const bf16_t* __restrict__ w, const float* __restrict__ s,
                                                                 const float* __restrict__ P, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float* __restrict__ stats,
-                                                                float* __restrict__ save, float* __restrict__ aff, int C,
-                                                                int p, float inv_m, float eps) {
+                                                                float* __restrict__ save, float* __restrict__ aff,
+                                                                const float* __restrict__ add_shift, int C, int p,
+                                                                float inv_m, float eps) {
     const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (o >= C) return;  // wave-uniform
     float m1 = 0.f, m2 = 0.f;
@@ -161,33 +208,35 @@ __global__ __launch_bounds__(256) void bn_gram_fwd_stats_kernel(const bf16_t* __
     m1 = wave_sum(m1) * inv_m;
     m2 = wave_sum(m2) * inv_m;
     if (lane) return;
-    const float var = fmaxf(m2 - m1 * m1, 0.f), rstd = rsqrtf(var + eps), sc = gamma[o] * rstd;
+    const float var = fmaxf(m2, 0.f), rstd = rsqrtf(var + eps), sc = gamma[o] * rstd;
     stats[o] = m1;
     stats[C + o] = var;
     save[o] = m1;
     save[C + o] = rstd;
     aff[o] = sc;
-    aff[C + o] = beta[o] - m1 * sc;
+    aff[C + o] = beta[o] - m1 * sc + (add_shift ? add_shift[o] : 0.f);
 }
 
 }  // namespace
 
+// add_shift (may be null): added to the epilogue shift (a downsample block's shortcut-BN shift, folded into bn3's)
 IMK_EXPORT int imk_bn_gram_fwd_stats(const void* w, const float* s, const float* P, const float* gamma,
-                                     const float* beta, float* stats, float* save, float* aff, long M, int C, int p,
-                                     float eps, void* stream) {
+                                     const float* beta, float* stats, float* save, float* aff, const float* add_shift,
+                                     long M, int C, int p, float eps, void* stream) {
     if (M <= 0 || C <= 0 || p <= 0) return -100;
     hipLaunchKernelGGL(bn_gram_fwd_stats_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)w, s, P, gamma, beta, stats, save, aff, C, p, 1.f / (float)M, eps);
+                       (const bf16_t*)w, s, P, gamma, beta, stats, save, aff, add_shift, C, p, 1.f / (float)M, eps);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
-IMK_EXPORT int imk_bn_bwd_coef_T(const float* scratch, const float* T, const void* w, const float* save,
-                                 const float* gamma, float* dgamma_acc, float* dbeta_acc, float* coef, long R, int C,
-                                 int p, void* stream) {
+IMK_EXPORT int imk_bn_bwd_coef_T(const float* scratch, const float* T, const void* w, const float* hs,
+                                 const float* save, const float* gamma, float* dgamma_acc, float* dbeta_acc,
+                                 float* coef, long R, int C, int p, void* stream) {
     if (R <= 0 || C <= 0 || p <= 0) return -100;
     hipLaunchKernelGGL(bn_bwd_coef_T_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, scratch, T,
-                       (const bf16_t*)w, save, gamma, dgamma_acc, dbeta_acc, coef, BWD_SLOTS_G, C, p, 1.f / (float)R);
+                       (const bf16_t*)w, hs, save, gamma, dgamma_acc, dbeta_acc, coef, BWD_SLOTS_G, C, p,
+                       1.f / (float)R);
     IMK_CHECK_LAUNCH();
     return 0;
 }
@@ -210,21 +259,32 @@ IMK_EXPORT int imk_bn_gram_dgrad_weights(const void* wt, int ldw, const float* c
     return 0;
 }
 
+// Q = W3^T diag(B) W3 [p][p] (wt = W3^T [p][ldw] bf16)
 IMK_EXPORT int imk_bn_gram_q(const void* wt, int ldw, const float* coef, float* Q, int p, int C4, void* stream) {
-    if (p <= 0 || p % 16 || C4 <= 0 || ldw < C4) return -100;
-    hipLaunchKernelGGL(bn_gram_q_kernel, dim3(p / 16, p / 16), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)wt,
-                       ldw, coef, Q, p, C4);
+    if (p <= 0 || p % 64 || C4 <= 0 || C4 % 16 || ldw < C4) return -100;
+    hipLaunchKernelGGL(bn_gram_gemm_kernel<1>, dim3(p / 64, p / 64), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)wt, ldw, nullptr, nullptr, coef, Q, p, p, C4, 0.f);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
-IMK_EXPORT int imk_bn_gram_wgrad_fixup(float* dw, const float* T, const float* P, const float* coef, const float* s,
-                                       int C4, int p, void* stream) {
+// P = W3 (G - s s^T / rows) [C4][p] (W3 [C4][p] bf16, G [p][p], s [p])
+IMK_EXPORT int imk_bn_gram_p(const void* w, const float* G, const float* s, float* P, long rows, int C4, int p,
+                             void* stream) {
+    if (rows <= 0 || p <= 0 || p % 64 || C4 <= 0 || C4 % 64) return -100;
+    hipLaunchKernelGGL(bn_gram_gemm_kernel<0>, dim3(p / 64, C4 / 64), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)w, p, G, s, nullptr, P, C4, p, p, 1.f / (float)rows);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_bn_gram_wgrad_fixup(float* dw, const float* T, const float* P, const float* coef,
+                                       const float* mean, const float* s, int C4, int p, void* stream) {
     if (p <= 0 || C4 <= 0) return -100;
     const long n = (long)C4 * p;
     const int grid = (int)std::min<long>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(bn_gram_wgrad_fixup_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dw, T, P, coef, s,
-                       C4, p);
+    hipLaunchKernelGGL(bn_gram_wgrad_fixup_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dw, T, P, coef,
+                       mean, s, C4, p);
     IMK_CHECK_LAUNCH();
     return 0;
 }

@@ -346,21 +346,14 @@ int halo_cus() {
     return n;
 }
 
-// IMAGENT_HALO_BLOCKS: blocks per CU (default 1: one persistent block per CU)
-int halo_blocks_per_cu() {
-    static const int n = [] {
-        const char* e = getenv("IMAGENT_HALO_BLOCKS");
-        const int v = e ? atoi(e) : 1;
-        return v < 1 ? 1 : v;
-    }();
-    return n;
-}
+// blocks per CU: one persistent block per CU (2 measured within noise, round-4 switch sweep)
+constexpr int HALO_BLOCKS_PER_CU = 1;
 
 template <int W, int R, int EPI>
 int launch_halo(const IGemmArgs& a, hipStream_t st) {
     const size_t lds = halo_lds(W, R);
     const int nbands = a.N * (a.H / R);
-    const int G = std::min(nbands, halo_cus() * halo_blocks_per_cu());
+    const int G = std::min(nbands, halo_cus() * HALO_BLOCKS_PER_CU);
     hipLaunchKernelGGL((halo3x3_kernel<W, R, EPI>), dim3(G), dim3(512), lds, st, a, nbands);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
@@ -373,11 +366,6 @@ bool tap_in_halo(int d0, int ds) { return d0 >= -1 && d0 <= 1 && d0 + 2 * ds >= 
 
 // Returns 1 when the shape / flags are not the halo kernel's (caller falls back).
 int conv_halo(const IGemmArgs& a, hipStream_t st) {
-    static const bool on = [] {
-        const char* e = getenv("IMAGENT_HALO");
-        return !e || e[0] != '0';
-    }();
-    if (!on) return 1;
     if (a.flags & (IG_OUT_F32 | IG_STEM | IG_REGSTAGE | IG_FP8 | IG_ACCUM_SUB2)) return 1;
     // the eval forward's folded BatchNorm (+ ReLU after the optional accumulate): plain epilogue only
     if ((a.flags & (IG_AFFINE | IG_RELU)) && ((a.flags & IG_BNBWD) || a.stats || a.xbn)) return 1;

@@ -3,7 +3,6 @@
 
 #include "conv_igemm_impl.h"
 #include "conv_igemm_v3.h"
-#include "conv_igemm_v4.h"
 
 // Tile selection (auto, tile 0):
 //  * 64 -> 64 3x3 stride 1: the halo-tiled kernel (conv_halo.hip);
@@ -20,44 +19,20 @@
 // r50_conv_phased_kernel.md), the ping-pong 256x256 kernel after the 8-phase template (-3.2 %),
 // static wave priority for the second half of the waves (neutral).
 
-// Wave-quantisation tail of the one-tile-per-block 256x256 kernels (one block per CU): with
-// T tiles on S CUs the last of ceil(T / S) rounds runs T mod S tiles on an otherwise idle chip
-// (R50 at 1024 img: 784 tiles on 256 CUs = 3 rounds + 16 tiles for every N = 256 conv at 14x14).
-// When that remainder is a small fraction of S, the conv is split at an IMAGE boundary: the
-// first I1 images fill exactly the whole rounds with 256x256 tiles, the remaining images run as
-// 128x128 tiles (4x as many blocks, one quarter of the work each) right after. Every pixel-
-// indexed operand advances by whole images; the statistics slabs accumulate across both
-// launches. IMAGENT_IGEMM_TAIL=0 disables, 1 splits every such conv, 2 only those without a
-// fused BN-backward / accumulating epilogue (the forward convs: in backward the weight-gradient
-// side stream already fills the idle CUs of the last round); IMAGENT_IGEMM_TAIL_FRAC sets the
-// largest remainder fraction that is split (default 0.3).
-static int tail_mode() {
-    static const int m = [] {
-        const char* e = getenv("IMAGENT_IGEMM_TAIL");
-        return e ? atoi(e) : 2;
-    }();
-    return m;
-}
+// Smallest K (= taps x C) that takes the 256x256 v3 tile (one block per CU); below it the 128x128 tile (two blocks
+// per CU) overlaps one block's epilogue with the other's main loop, which is what the epilogue-heavy short-K
+// BN-backward dgrads need (A/B at batch 1024: 12,782 img/s with every conv on the big tile, 12,872 at 512)
+constexpr int V3_BIG_MIN_K = 512;
 
-static float tail_frac() {
-    static const float f = [] {
-        const char* g = getenv("IMAGENT_IGEMM_TAIL_FRAC");
-        return g ? (float)atof(g) : 0.3f;
-    }();
-    return f;
-}
-
-// IMAGENT_V3_256_MINK: smallest K (= taps x C) that takes the 256x256 v3 tile (one block per CU); below
-// it the 128x128 tile (two blocks per CU) overlaps one block's epilogue with the other's main loop,
-// which is what the epilogue-heavy short-K BN-backward dgrads need (A/B: scripts/gpu_ab_v3.sh)
-static int v3_big_min_k() {
-    static const int v = [] {
-        const char* e = getenv("IMAGENT_V3_256_MINK");
-        return e ? atoi(e) : 512;  // A/B at batch 1024: 0 -> 12,782, 512 -> 12,872 img/s
-    }();
-    return v;
-}
-
+// Wave-quantisation tail of the one-tile-per-block 256x256 kernels (one block per CU): with T tiles on S CUs the
+// last of ceil(T / S) rounds runs T mod S tiles on an otherwise idle chip (R50 at 1024 img: 784 tiles on 256 CUs =
+// 3 rounds + 16 tiles for every N = 256 conv at 14x14). When that remainder is at most 30 % of S, a FORWARD conv
+// (no fused BN-backward / accumulating epilogue: in backward the weight-gradient side stream already fills the
+// idle CUs of the last round) is split at an IMAGE boundary: the first I1 images fill exactly the whole rounds
+// with 256x256 tiles, the remaining images run as 128x128 tiles (4x as many blocks, one quarter of the work each)
+// right after. Every pixel-indexed operand advances by whole images; the statistics slabs accumulate across both
+// launches.
+constexpr float TAIL_FRAC = 0.3f;
 static int device_cus() {
     static const int n = [] {
         int dev = 0, cus = 0;
@@ -71,16 +46,13 @@ static int device_cus() {
 
 // images of the main part, or 0 when the conv is not split
 static int tail_split_images(const IGemmArgs& a) {
-    const int mode = tail_mode();
-    const float frac = tail_frac();
-    if (mode == 0 || frac <= 0.f || a.N < 2) return 0;
-    if (mode == 2 && (a.flags & (IG_BNBWD | IG_ACCUM))) return 0;
+    if (a.N < 2 || (a.flags & (IG_BNBWD | IG_ACCUM))) return 0;
     const long ohw = (long)a.OH * a.OW;
     const long nbn = (a.Nout + 255) / 256;
     const long tiles = ((a.M + 255) / 256) * nbn;
     const long S = device_cus();
     const long full = tiles / S, rem = tiles - full * S;
-    if (full < 1 || rem == 0 || rem > frac * S) return 0;
+    if (full < 1 || rem == 0 || rem > TAIL_FRAC * S) return 0;
     const long mt = full * S / nbn;           // M tiles the whole rounds hold
     const long i1 = mt * 256 / ohw;           // whole images inside them
     return (i1 >= 1 && i1 < a.N) ? (int)i1 : 0;
@@ -128,12 +100,9 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         return conv_stream(a, st);
     }
     if (a.X2) {  // two K segments (bn_gram.hip): the streaming kernel for 256 + 64 -> 64, else the v3 loop
-        // IMAGENT_GRAM_STREAM=0: the v3 loop for every shape (A/B)
-        static const bool gstream = [] {
-            const char* e = getenv("IMAGENT_GRAM_STREAM");
-            return !e || atoi(e) != 0;
-        }();
-        if (tile == 0 && gstream) {
+        // (the streaming kernel where it takes the shape: 963 vs 1087 us per call in-step for the layer-1 form;
+        // tile != 0 forces the v3 loop, tests / A/B)
+        if (tile == 0) {
             const int r = conv_stream(a, st);
             if (r != 1) return r;
         }
@@ -153,15 +122,6 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // short-K 1x1 convs (K = C = 64 / 128) are HBM streams: weights resident in
     // LDS, pixel fragments straight from HBM (conv_stream.hip); tiles 20/21/22
     // force its 256/128/64-channel slices (A/B testing)
-    if (tile >= 30 && tile <= 33) {  // v4 main loop (conv_igemm_v4.h): one 4-wave block per CU
-        if (!v4_ok(a) || (a.flags & (IG_OUT_F32 | IG_RELU | IG_EPI_DIRECT))) return -105;
-        switch (tile) {
-            case 30: return launch_v4<256, 256, 2, 4, 64, 32>(a, st);
-            case 31: return launch_v4<256, 256, 2, 3, 64, 32>(a, st);
-            case 32: return launch_v4<256, 128, 2, 4, 64, 32>(a, st);
-            default: return launch_v4<128, 256, 2, 4, 64, 32>(a, st);
-        }
-    }
     const int bn_hint = tile >= 20 && tile <= 22 ? 256 >> (tile - 20) : 0;
     if (tile >= 20 && tile <= 22) tile = 0;
     const bool autotile = tile == 0;
@@ -203,7 +163,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
         // (the fused BN-backward dgrads on 128x128 tiles with their epilogue operands prefetched instead: within
         // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken)
-        if (a.Nout >= 512 && t8 >= 192 && K >= v3_big_min_k()) {
+        if (a.Nout >= 512 && t8 >= 192 && K >= V3_BIG_MIN_K) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles
                 IGemmArgs m = a, t = a;

@@ -533,27 +533,10 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     }
     int maxbn = (a.C == 64 && !(a.flags & IG_BNBWD)) ? 256 : 128;
     if (a.flags & IG_BNBWD) {
-        // BN-backward epilogue: IMAGENT_STREAM_BNB = all (default: every K = 64 / 128 / 256 dgrad, with or
-        // without the second BN branch), 0 (never), 64 / 128 (slice width; K = 64 / 256 without the second
-        // branch only), x2 (the latter + K = 64 with the second branch). Same-box bench A/B at R50 / 1024 with
-        // the ReLU mask as bits (round 3): all 73.9 ms/step vs 75.2 for 128 and 75.0 for x2 (the round-1
-        // measurement that kept K = 128 and the second branch on the tiled kernels predates the bit mask
-        // and the register-light BN epilogue)
-        static const int pref = [] {
-            const char* e = getenv("IMAGENT_STREAM_BNB");
-            return !e || e[0] == 'a' || e[0] == 'x' ? 128 : atoi(e);
-        }();
-        if (pref == 0) return 1;
-        static const bool all = [] {
-            const char* e = getenv("IMAGENT_STREAM_BNB");
-            return !e || e[0] == 'a';
-        }();
-        static const bool x2 = [] {
-            const char* e = getenv("IMAGENT_STREAM_BNB");
-            return e && e[0] == 'x';
-        }();
-        if (!all && ((a.C != 64 && a.C != 256) || (a.bnx2 && !(x2 && a.C == 64)))) return 1;
-        maxbn = (pref >= 128 || all) ? 128 : 64;
+        // BN-backward epilogue: every K = 64 / 128 / 256 dgrad, with or without the second BN branch, 128-channel
+        // slices. Same-box bench A/B at R50 / 1024 with the ReLU mask as bits (round 3): 73.9 ms/step vs 75.2 with
+        // K = 128 on the tiled kernels and 75.0 with the second branch there too; 64-channel slices neutral
+        maxbn = 128;
     }
     if (bn == 0) bn = maxbn;
     while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
@@ -568,12 +551,8 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     }
     // K = 256 BN-backward dgrads into wide outputs (bottleneck conv1 dgrads 256 -> 512 @28, 256 -> 1024 @14): 64-channel
     // weight slices resident in LDS (as the K = 256 forwards) instead of the one-tile-per-block v3 loop, whose
-    // 4-stage main loop leaves these epilogue-heavy GEMMs latency-bound. IMAGENT_STREAM_BNB256=0: v3 (A/B)
-    static const bool bnb256 = [] {
-        const char* e = getenv("IMAGENT_STREAM_BNB256");
-        return !e || atoi(e) != 0;
-    }();
-    if (a.C == 256 && (a.flags & IG_BNBWD) && a.Nout > 128 && bnb256) {
+    // 4-stage main loop leaves these epilogue-heavy GEMMs latency-bound (-20 % per call, round 4)
+    if (a.C == 256 && (a.flags & IG_BNBWD) && a.Nout > 128) {
         if (a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 3>(a, st) : 1;
         return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
     }

@@ -262,17 +262,12 @@ int launch1(WgradArgs a, int splits, hipStream_t st) {
     if (splits <= 0) {
         // ~3 blocks per CU over 256 CUs (4-wave blocks, 2 resident per CU) or
         // ~2 (8-wave blocks, 1 resident), at least 4 stages per block
-        static const int tgt_env = [] {
-            const char* e = getenv("IMAGENT_WGRAD_TARGET");
-            return e ? atoi(e) : 0;
-        }();
         // measured (conv_bench, R50 at 1024 img): the stem and the <= 128-channel 3x3 convs
         // (few tiles, latency-bound staging) gain from 4-5 blocks per CU (stem 1108 -> 944 us,
         // 64@56 3x3 630 -> 577, 128@28 3x3 502 -> 461); 1x1 convs lose (more split-K atomics)
         int target = NW == 4 ? 768 : 512;
         if (NW == 4 && STEM) target = 1280;
         else if (NW == 4 && a.KH * a.KW > 1 && a.Ci <= 128) target = 1024;
-        if (tgt_env > 0) target = tgt_env;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));
@@ -332,14 +327,13 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
             default: return launch_wgrad_v3<64, 2>(a, splits, st);
         }
     }
-    // 3x3 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
-    // 1 only 64 -> 64, 2 (default) every stride-1 shape it covers, 3 also the stride-2 phase-plane form (measured
-    // slower than the register-staged kernel on every R50 stride-2 shape, profiles/r50_b1024_round4_kernel_ab.md)
+    // 3x3 stride-1 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
+    // 1 only 64 -> 64, 2 (default) every shape it covers
     static const int halo = [] {
         const char* e = getenv("IMAGENT_WGRAD_HALO");
         return e ? atoi(e) : 2;
     }();
-    if (halo && (a.stride == 1 || halo >= 3) && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
+    if (halo && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
     // 2 % slower than this register-staged loop on every R50 shape: not kept)

@@ -28,16 +28,9 @@
 // 585 -> 275 us, 128@28 462 -> 306, 256@14 402 -> 271 (870 TFLOP/s); 512@7 390 vs 364 for the
 // register-staged kernel (2 k-steps per band, 23 % zero padding): not the default there.
 //
-// Stride 2 (S = 2; the bottlenecks' strided 3x3 convs 128@56 -> 28, 256@28 -> 14, 512@14 -> 7): output pixel
-// (oy, ox) reads input (2 oy + ti - 1, 2 ox + tj - 1), so consecutive output pixels are NOT consecutive input
-// pixels. The patch is staged as the four PHASE planes of the input (row parity py, column parity px): plane
-// (py, px) row r, column c holds input (2 (y0 + r) - 1 + py, 2 c - 1 + px), R + 1 rows of PW pixels each. Tap
-// (ti, tj) is then the plane (ti & 1, tj & 1) shifted by (ti >> 1, tj >> 1) -- a window of consecutive pixels
-// again, with the row / plane offsets multiples of 8 rows (swizzle kept, immediate offsets). (OW, R) in
-// {(28, 2), (14, 2), (7, 7)}; W here is the OUTPUT width. Measured at R50 / batch 1024 (isolated): 128@56 s2
-// 501 vs 456 us for the register-staged kernel, 256@28 620 vs 440, 512@14 461 vs 402 -- the two-row bands the
-// 160-KB LDS allows stage 4 input pixels per output pixel for 1-2 k-steps each, so the DMA / barrier per band
-// is not amortised: opt-in only (IMAGENT_WGRAD_HALO=3).
+// (A stride-2 form that staged the four phase planes of the input measured slower than the register-staged
+// kernel on every R50 stride-2 shape -- 128@56 s2 501 vs 456 us, 256@28 620 vs 440, 512@14 461 vs 402 -- and
+// was removed in round 5; profiles/r50_b1024_round4_kernel_ab.md.)
 
 #pragma once
 
@@ -54,18 +47,16 @@ __device__ __forceinline__ int wh_swz(int q) { return (q >> 1) & 3; }
 // physical 16-B chunk slot of logical chunk c (0..7) of row q (and its inverse: the map is an involution)
 __device__ __forceinline__ int wh_slot(int c, int q) { return (((c >> 1) ^ wh_swz(q)) << 1) | (c & 1); }
 
-template <int W, int R, int NKS, int PW, int S = 1>
+template <int W, int R, int NKS, int PW>
 __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, int nbands, int nranges) {
     constexpr int BP = R * W;           // band pixels (NKS x 32 rows staged: the rest are zero dY rows)
-    constexpr int PR = S == 1 ? R + 2 : R + 1;  // patch rows (per phase plane for S = 2)
-    constexpr int NPL = S == 1 ? 1 : 4;         // phase planes
+    constexpr int PR = R + 2;           // patch rows
     constexpr int DYB = NKS * 32 * 128; // dY image bytes
-    constexpr int PB = NPL * PR * PW * 128;     // patch image bytes
+    constexpr int PB = PR * PW * 128;   // patch image bytes
     constexpr int BUF = DYB + PB;
     constexpr int NDY = DYB / 1024, NP = NDY + PB / 1024;
     constexpr int PPW = (NP + 3) / 4;   // DMA pieces per wave per band
-    static_assert(S == 1 || S == 2, "stride");
-    static_assert(PW % 8 == 0 && W + (S == 1 ? 2 : 1) <= PW && BP <= NKS * 32 && NKS * 32 - BP < 32 &&
+    static_assert(PW % 8 == 0 && W + 2 <= PW && BP <= NKS * 32 && NKS * 32 - BP < 32 &&
                       (PR * PW) % 8 == 0 && NP - 3 * PPW >= 0,
                   "band geometry");
     static_assert(2 * BUF <= 160 * 1024, "two band buffers in LDS");
@@ -105,17 +96,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
                                                          0, 0);
             } else {
                 const int q = (piece - NDY) * 8 + drow;  // patch row index
-                int iy, ix;
-                if (S == 1) {
-                    const int pr = q / PW, pc = q - pr * PW;
-                    iy = y0 - 1 + pr;
-                    ix = pc - 1;
-                } else {  // phase plane (py, px), row pr, column pc
-                    const int pl = q / (PR * PW), rq = q - pl * (PR * PW);
-                    const int pr = rq / PW, pc = rq - pr * PW;
-                    iy = 2 * (y0 + pr) - 1 + (pl >> 1);
-                    ix = 2 * pc - 1 + (pl & 1);
-                }
+                const int pr = q / PW, pc = q - pr * PW;
+                const int iy = y0 - 1 + pr, ix = pc - 1;
                 uint32_t off = WH_OOB;
                 if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
                     off = ((uint32_t)(img * a.H + iy) * a.W + (uint32_t)ix) * ldx + (uint32_t)(wh_slot(dslot, q) * 16);
@@ -138,11 +120,10 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
 #pragma unroll
             for (int i = 0; i < 4; ++i) adA[ks][r][i] = (uint32_t)(P * 128 + ((i ^ wh_swz(P)) << 5) + 8 * p4);
             const int Pp = P < BP ? P : 0;  // a padded k row (zero dY) reads any patch row: 0 x finite
-            const int Q0 = (Pp / W) * PW + (Pp % W);  // patch row of tap (0, 0) (of plane (0, 0) for S = 2)
+            const int Q0 = (Pp / W) * PW + (Pp % W);  // patch row of tap (0, 0)
 #pragma unroll
             for (int tj = 0; tj < 3; ++tj) {
-                // S = 2: column parity plane tj & 1, shifted by tj >> 1
-                const int q = S == 1 ? Q0 + tj : (tj & 1) * PR * PW + Q0 + (tj >> 1);
+                const int q = Q0 + tj;
                 adB[ks][r][tj] = (uint32_t)(DYB + q * 128 + ((wid ^ wh_swz(q)) << 5) + 8 * p4);
             }
         }
@@ -181,10 +162,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
             for (int ti = 0; ti < 3; ++ti)
 #pragma unroll
                 for (int tj = 0; tj < 3; ++tj) {
-                    // tap row: S = 1 shifts by ti rows; S = 2 selects the row parity plane (ti & 1: planes 2, 3)
-                    // and shifts by ti >> 1 rows
-                    constexpr int PLB = 2 * PR * PW * 128;
-                    const int toff = S == 1 ? ti * PW * 128 : (ti & 1) * PLB + (ti >> 1) * PW * 128;
+                    const int toff = ti * PW * 128;  // tap row: the window shifted by ti patch rows
                     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (LDS_PTR(s16x4))(base + adB[ks][0][tj] + toff));
                     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -220,11 +198,6 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
 inline bool wgrad_halo_ok(const WgradArgs& a, bool wide = true, bool dflt = false) {
     if (a.stem || a.xbn) return false;
     if (a.Ci % 64 || a.Co % 64 || a.KH != 3 || a.KW != 3 || a.pad != 1) return false;
-    if (a.stride == 2) {  // phase-plane patch: even input sizes, (OW, R) in {(28, 2), (14, 2), (7, 7)}
-        if (!wide || a.H != 2 * a.OH || a.W != 2 * a.OW) return false;
-        const bool geo = (a.OW == 28 && a.OH % 2 == 0) || (a.OW == 14 && a.OH % 2 == 0) || (a.OW == 7 && a.OH % 7 == 0);
-        return geo && (size_t)a.N * a.H * a.W * a.Ci * 2 < (1ull << 31) && (size_t)a.M * a.Co * 2 < (1ull << 31);
-    }
     if (a.stride != 1) return false;
     if (!wide && (a.Ci != 64 || a.Co != 64)) return false;
     if (a.OW != a.W || a.OH != a.H) return false;
@@ -235,7 +208,7 @@ inline bool wgrad_halo_ok(const WgradArgs& a, bool wide = true, bool dflt = fals
     return geo && (size_t)a.N * a.H * a.W * a.Ci * 2 < (1ull << 31) && (size_t)a.M * a.Co * 2 < (1ull << 31);
 }
 
-template <int W, int R, int NKS, int PW, int S = 1>
+template <int W, int R, int NKS, int PW>
 int launch_wgrad_halo1(const WgradArgs& a, hipStream_t st) {
     const int nbands = a.N * (a.OH / R);
     static int cus = 0;
@@ -248,8 +221,8 @@ int launch_wgrad_halo1(const WgradArgs& a, hipStream_t st) {
     const int npairs = (a.Co / 64) * (a.Ci / 64);
     // ~one block per CU (LDS-bound residency), at least one band per range
     const int nranges = std::max(1, std::min(nbands, (cus + npairs - 1) / npairs));
-    const size_t lds = 2 * ((size_t)NKS * 32 * 128 + (S == 1 ? (size_t)(R + 2) : 4 * (size_t)(R + 1)) * PW * 128);
-    hipLaunchKernelGGL((wgrad_halo_kernel<W, R, NKS, PW, S>), dim3(nranges * npairs), dim3(256), lds, st, a, nbands,
+    const size_t lds = 2 * ((size_t)NKS * 32 * 128 + (size_t)(R + 2) * PW * 128);
+    hipLaunchKernelGGL((wgrad_halo_kernel<W, R, NKS, PW>), dim3(nranges * npairs), dim3(256), lds, st, a, nbands,
                        nranges);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
@@ -257,14 +230,6 @@ int launch_wgrad_halo1(const WgradArgs& a, hipStream_t st) {
 }
 
 inline int launch_wgrad_halo(const WgradArgs& a, hipStream_t st) {
-    if (a.stride == 2) {
-        switch (a.OW) {
-            case 28: return launch_wgrad_halo1<28, 2, 2, 32, 2>(a, st);
-            case 14: return launch_wgrad_halo1<14, 2, 1, 16, 2>(a, st);
-            case 7: return launch_wgrad_halo1<7, 7, 2, 8, 2>(a, st);
-            default: return -106;
-        }
-    }
     switch (a.W) {
         case 56: return launch_wgrad_halo1<56, 4, 7, 64>(a, st);
         case 28: return launch_wgrad_halo1<28, 4, 4, 32>(a, st);

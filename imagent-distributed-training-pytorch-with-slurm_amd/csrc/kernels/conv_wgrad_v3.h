@@ -197,15 +197,10 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
     const int K = a.KH * a.KW * a.Ci;
     const int ntiles = (a.Co / 128) * (K / 128);
     if (splits <= 0) {
-        static const int tgt_env = [] {
-            const char* e = getenv("IMAGENT_WGRAD_V3_TARGET");
-            if (!e) e = getenv("IMAGENT_WGRAD_TARGET");
-            return e ? atoi(e) : 0;
-        }();
         // one wave of 2 blocks per CU over 256 CUs: the 1x1 wgrads are split-K streams whose second, partial
         // wave of blocks cost more than the extra atomics of deeper splits save (same-box bench: 512 blocks
-        // 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282; IMAGENT_WGRAD_V3_TARGET)
-        const int target = tgt_env > 0 ? tgt_env : 512;
+        // 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282)
+        constexpr int target = 512;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));

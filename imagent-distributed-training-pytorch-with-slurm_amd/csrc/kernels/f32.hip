@@ -979,13 +979,9 @@ IMK_EXPORT int imk_conv_f32(const IGemmArgs* args, void* stream) {
     if (a.C % 4 || (a.flags & ~(IG_ACCUM | IG_OUT_F32 | IG_BNBWD))) return -100;
     const int ntiles = ((a.M + F_BM - 1) / F_BM) * ((a.Nout + F_BN - 1) / F_BN);
     const size_t lds = 2 * (F_BM + F_BN) * F_BK * sizeof(float);  // (= the split kernel's 2 x 4 bf16 planes)
-    // split arithmetic, C % 32 == 0: the v3 LDS-DMA ring with fp32 rows (conv_igemm_v3.h, EB = 4; IMAGENT_F32_V3=0:
-    // the register-staged kernel below, A/B)
-    static const bool v3 = [] {
-        const char* e = getenv("IMAGENT_F32_V3");
-        return !e || atoi(e) != 0;
-    }();
-    if (g_f32_split && v3 && v3_ok32(a)) {
+    // split arithmetic, C % 32 == 0: the v3 LDS-DMA ring with fp32 rows (conv_igemm_v3.h, EB = 4); the register-
+    // staged kernel below for the rest
+    if (g_f32_split && v3_ok32(a)) {
         const int r = a.Nout <= 64 ? launch_v3<128, 64, 1, 2, 4, 128, 4>(a, (hipStream_t)stream)
                                    : launch_v3<128, 128, 2, 2, 4, 128, 4>(a, (hipStream_t)stream);
         return r;

@@ -378,13 +378,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
     }
 }
 
-// IMAGENT_POOL_QUAD=0: the per-pixel backward kernel for the stem pool too (A/B)
+// the stem pool's quad-gather backward covers 3x3 / stride 2 / pad 1 on even inputs
 bool pool_quad_ok(int H, int W, int OH, int OW, int k, int s, int p) {
-    static const bool on = [] {
-        const char* e = getenv("IMAGENT_POOL_QUAD");
-        return !e || e[0] != '0';
-    }();
-    return on && k == 3 && s == 2 && p == 1 && H == 2 * OH && W == 2 * OW;
+    return k == 3 && s == 2 && p == 1 && H == 2 * OH && W == 2 * OW;
 }
 
 // ------------------------------------------------------------------ avgpool
@@ -746,6 +742,37 @@ IMK_EXPORT int imk_xent_bwd(const float* logits, const int64_t* labels, const fl
     hipLaunchKernelGGL(xent_bwd_kernel, dim3((NC + 255) / 256, B), dim3(256), 0, (hipStream_t)stream,
                        logits, labels, lse, gout, (bf16_t*)dz, B, NC, smoothing);
     IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// The stem's weight gradient from its row-segment layout gp [Co][KH][32] (channel-padded 4-channel pixels, kw * 4 +
+// ci) into the master gradient [Co][Ci][KH][KW] (+=, gradient accumulation), clearing gp for the next step's
+// atomic accumulation in the same pass (one launch instead of a fill + a strided add).
+__global__ __launch_bounds__(256) void stem_grad_fold_kernel(float* __restrict__ gp, float* __restrict__ grad, int Co,
+                                                             int Ci, int KH, int KW) {
+    const int n = Co * Ci * KH * KW;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+        const int kw = e % KW, kh = (e / KW) % KH, ci = (e / (KW * KH)) % Ci, co = e / (KW * KH * Ci);
+        float* src = gp + ((size_t)co * KH + kh) * 32 + kw * 4 + ci;
+        grad[e] += *src;
+        *src = 0.f;
+    }
+}
+
+IMK_EXPORT int imk_stem_grad_fold(float* gp, float* grad, int Co, int Ci, int KH, int KW, void* stream) {
+    if (Co <= 0 || Ci <= 0 || Ci > 4 || KW * 4 > 32 || KH <= 0) return -100;
+    const int n = Co * Ci * KH * KW;
+    hipLaunchKernelGGL(stem_grad_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, gp, grad,
+                       Co, Ci, KH, KW);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+// Zero a device buffer on a stream (the per-step gradient arena / workspace clears): one hipMemsetAsync (a runtime
+// fill, not an ATen FillFunctor launch).
+IMK_EXPORT int imk_memset0(void* p, long bytes, void* stream) {
+    if (!p || bytes < 0) return -100;
+    if (bytes && hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream) != hipSuccess) return -1;
     return 0;
 }
 

@@ -109,7 +109,8 @@ class ParamArena:
         return out
 
     def zero_grad(self) -> None:
-        self.G.zero_()
+        from ..ops import _lib
+        _lib.zero_(self.G)
 
     def bucket_param_order(self) -> List[int]:
         return list(self.order)

@@ -305,9 +305,9 @@ def _conv(x, conv: Conv2d, bn: Optional[BatchNorm2d], train: bool):
                      stem=getattr(conv, "stem", False))
 
 
-# IMAGENT_STEM_FUSE=0: the stem's BN+ReLU and maxpool as separate autograd
-# nodes (pool backward, BN reduce, BN apply) -- A/B switch
-_FUSED_STEM = os.environ.get("IMAGENT_STEM_FUSE", "1") != "0"
+# the stem's BN+ReLU and maxpool as one autograd node (ops.misc.BNReluPoolFn: BN applied inside the pool forward,
+# the BN-backward reductions carried by the pool backward); the deterministic mode keeps separate nodes
+_FUSED_STEM = True
 
 
 def _bn(x, bn, relu, train, x2=None, bn2=None, mode=0):
@@ -324,7 +324,7 @@ def forward_hip(model: ResNet, x: torch.Tensor) -> torch.Tensor:
                          f"{tuple(x.shape)} {x.dtype}")
     train = model.training and torch.is_grad_enabled()
     if train:
-        st.zero_ws.zero_()
+        _lib.zero_(st.zero_ws)
     q = st.fp8 if (train and st.fused_blocks) else None
     if q is not None:
         q.begin_forward()

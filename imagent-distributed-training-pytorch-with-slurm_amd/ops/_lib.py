@@ -166,7 +166,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
                            vp, vp, vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
-            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, vp],
+            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_eval_affine": [vp, i32, vp],
             "imk_set_deterministic": [i32],
@@ -184,12 +184,15 @@ def _declare(name: str, lib) -> None:
             "imk_xent_fwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_xent_bwd": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_colsum_bf16": [vp, vp, i32, i32, vp],
-            "imk_bn_bwd_coef_T": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
-            "imk_bn_gram_fwd_stats": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, f32, vp],
+            "imk_stem_grad_fold": [vp, vp, i32, i32, i32, i32, vp],
+            "imk_memset0": [vp, i64, vp],
+            "imk_bn_bwd_coef_T": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
+            "imk_bn_gram_fwd_stats": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, f32, vp],
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_gram_dgrad_weights": [vp, i32, vp, vp, vp, vp, i32, i32, vp],
             "imk_bn_gram_q": [vp, i32, vp, vp, i32, i32, vp],
-            "imk_bn_gram_wgrad_fixup": [vp, vp, vp, vp, vp, i32, i32, vp],
+            "imk_bn_gram_wgrad_fixup": [vp, vp, vp, vp, vp, vp, i32, i32, vp],
+            "imk_bn_gram_p": [vp, vp, vp, vp, i64, i32, i32, vp],
             "imk_sgd": [vp, vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, f32, vp],
             "imk_cast_bf16": [vp, vp, i64, vp],
             "imk_uncast_bf16": [vp, vp, i64, vp],
@@ -282,6 +285,15 @@ def ptr(t) -> int:
 
 def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def zero_(t) -> None:
+    """t.zero_() for a contiguous device tensor as one hipMemsetAsync on the current stream (no ATen fill launch in
+    the training step); CPU / non-contiguous tensors: t.zero_()."""
+    if t.is_cuda and t.is_contiguous() and available():
+        check(kernels().imk_memset0(t.data_ptr(), t.numel() * t.element_size(), stream_ptr(t.device)), "memset")
+    else:
+        t.zero_()
 
 
 def check(rc: int, what: str) -> None:

@@ -37,15 +37,11 @@ from .bn_gram import GramBN, gram_T, gram_coef, gram_dgrad, gram_fwd_stats, gram
 from .conv import BNBwdFuse, conv_wgrad, igemm_dgrad, igemm_fwd
 
 
-# Issue each weight gradient after the BN-backward pass that follows its dgrad, so the side
-# stream's wgrad overlaps the next (compute-bound) dgrad rather than the memory-bound BN pass
-# (the two passes sharing HBM slowed the BN pass from 13 to 23 ms/step): measured +1.1 % img/s
-# at R50 / 1024 (12,131 vs 12,001). IMAGENT_DEFER_WGRAD=0: right after the dgrad (A/B switch).
-_DEFER_WGRAD = os.environ.get("IMAGENT_DEFER_WGRAD", "1") != "0"
-# IMAGENT_DS_SIDE=0: the downsample conv's forward on the main stream (A/B switch)
-_DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "1") != "0"
-# IMAGENT_SPARSE_DS=0: memset the stride-2 downsample dgrad's output (A/B switch)
-_SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
+# Each weight gradient is issued after the BN-backward pass that follows its dgrad, so the side stream's wgrad
+# overlaps the next (compute-bound) dgrad rather than the memory-bound BN pass (the two passes sharing HBM slowed
+# the BN pass from 13 to 23 ms/step): measured +1.1 % img/s at R50 / 1024 (12,131 vs 12,001). The downsample
+# conv's forward runs on the side stream beside the main chain's BN passes, and a stride-2 1x1 downsample dgrad
+# writes only the pixels it reaches (no memset; conv1's accumulating dgrad knows the rest are zero).
 # IMAGENT_BN_XFUSE (default 1; 0 = A/B off): a BatchNorm + ReLU inside a block whose consumer conv can
 # take it on its operand path is not a pass of its own: its statistics are finalized into a per-channel
 # scale / shift and the consumer applies them (+ ReLU) on its operand load -- the streaming 1x1 conv
@@ -57,7 +53,6 @@ _SPARSE_DS = os.environ.get("IMAGENT_SPARSE_DS", "1") != "0"
 # R18 448^2: the patch staging's extra VALU costs more than the skipped pass saves; opt-in)
 _XFUSE = os.environ.get("IMAGENT_BN_XFUSE", "1") != "0"
 _XFUSE_3X3 = os.environ.get("IMAGENT_BN_XFUSE", "1") == "all"
-_HALO = os.environ.get("IMAGENT_HALO", "1") != "0"
 # IMAGENT_BN_GRAM (default 1; 0 = A/B off): a bottleneck's last BatchNorm backward without its apply pass
 # (ops/bn_gram.py): conv3's dgrad runs over [g | h2] with folded weights, its wgrad from g^T h2 and the
 # Gram matrix of h2. conv3's input h2 is then kept (no operand-path BN fusion for that conv).
@@ -82,6 +77,8 @@ def _gram_ok(block, q, x) -> bool:
     pairs = block.convs_bns()
     if not (_GRAM and x.is_cuda and len(pairs) == 3):  # (with fp8: conv3's dgrad stays bf16 in this form)
         return False
+    if _conv.deterministic():  # split-K atomics accumulate G / T: never on the bit-identical statistics path
+        return False
     if not getattr(block, "_fuse_bnb", False):  # the next block's dgrad must reduce bn3 (premasked backward)
         return False
     c3 = pairs[-1][0]
@@ -101,7 +98,7 @@ def _xfuse_ok(conv, a, q) -> bool:
     H, W = a.shape[1], a.shape[2]
     # the halo kernel's launch conditions (conv_halo.hip, conv_halo()): W 56 with H % 4 == 0, or W 112 with
     # H % 2 == 0
-    return (_HALO and _XFUSE_3X3 and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
+    return (_XFUSE_3X3 and conv.kh == 3 and conv.kw == 3 and conv.stride == 1 and conv.padding == 1
             and conv.in_channels == 64 and conv.out_channels == 64
             and ((W == 56 and H % 4 == 0) or (W == 112 and H % 2 == 0)))
 
@@ -180,7 +177,7 @@ class BlockFn(torch.autograd.Function):
         ds = block.downsample
         # the downsample conv depends only on x: on the (idle in forward) side stream it
         # runs beside the main chain's memory-bound BN passes
-        side = streams.side_stream(x.device) if (ds is not None and _DS_SIDE and x.is_cuda) else None
+        side = streams.side_stream(x.device) if (ds is not None and x.is_cuda) else None
         ad = None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
@@ -215,13 +212,13 @@ class BlockFn(torch.autograd.Function):
         # bn3 + shortcut + ReLU in conv3's epilogue (x3 never materialised): a Gram-form block whose output mask
         # the next block's x-free dgrad epilogue reads, conv3 on the streaming kernel. A downsample block's
         # shortcut BN enters as a per-channel scale on the residual (its shift folded into bn3's)
-        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and fuse_next
+        # (the fused-output epilogue exists only on the streaming kernel: not with IMAGENT_CONV_STREAM=0)
+        fused3 = (gram and _GRAM_FWD and _GRAM_NOX and fuse_next and not _conv._NOSTREAM
                   and getattr(block, "_has_next", False) and gws is not None and h2sum is not None
                   and conv.in_channels in (64, 128, 256) and (ds is not None or x.shape[-1] == conv.out_channels))
         gram_P = None
         if fused3:
-            aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1])
-            res, rsc = x, None
+            res, rsc, ssd = x, None, None
             if ds is not None:
                 if side is not None:
                     cur = torch.cuda.current_stream()
@@ -230,8 +227,8 @@ class BlockFn(torch.autograd.Function):
                 else:
                     ad = _fwd8(ds[0], x, x8, ds[1])
                 ssd = bn_scale_shift(ad, ds[1])
-                aff[1] += ssd[1]
                 res, rsc = ad, ssd[0]
+            aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1], add_shift=ssd[1] if ssd is not None else None)
             out = torch.empty(res.shape, device=res.device, dtype=res.dtype)
             # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue; the output's
             # e4m3 copy from the same epilogue when an fp8 conv reads it
@@ -309,15 +306,10 @@ class BlockFn(torch.autograd.Function):
         if ds is not None:
             if premasked and ctx.gram and fuse:
                 # bn3 in the Gram form (as for identity blocks below); the downsample BN alone gets an apply pass:
-                # its reductions (sum g, sum g xhat_d) sit in bn3's slab rows 1, 2 -> its own rows 1, 0
+                # its reductions (sum g, sum g xhat_d) sit in bn3's slab rows 1, 2 (read there, sgx_row=2)
                 T = gram_T(dout, outs[-1], out=_gws(block, 0)) if getattr(block, "_bnb_nox", False) else None
-                dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
-                C3, S = out.shape[-1], _lib.STAT_SLOTS  # (the BN-backward slab has the statistics slab's depth)
-                src = bn_l.work.scratch[: S * 3 * C3].view(S, 3, C3)
-                dst = ds[1].work.scratch[: S * 3 * C3].view(S, 3, C3)
-                dst[:, 0].copy_(src[:, 2])
-                dst[:, 1].copy_(src[:, 1])
-                dAd, _ = bn_apply_backward(dout, ad, None, ds[1], None, 1)
+                dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None, hs=ctx.h2sum)
+                dAd, _ = bn_apply_backward(dout, ad, None, ds[1], None, 1, slab_of=bn_l, sgx_row=2)
                 dAd8 = None
             elif premasked:  # dout already masked + reduced by the next block's conv1 dgrad
                 g8a = q.grad_out(a_last, bn_l) if (q is not None and fp8_dgrad_ok(conv_l)) else None
@@ -330,7 +322,7 @@ class BlockFn(torch.autograd.Function):
             dconv = ds[0]
             # a stride-2 1x1 downsample reaches only the even pixels: write those, no memset of the
             # rest (conv1's dgrad below accumulates with old_sub2 = zeros at the odd ones)
-            sparse = _SPARSE_DS and dconv.stride == 2 and dconv.kh == 1 and dconv.kw == 1 and dconv.padding == 0
+            sparse = dconv.stride == 2 and dconv.kh == 1 and dconv.kw == 1 and dconv.padding == 0
             dX = igemm_dgrad(dAd, dconv.wt_bf16, (H, W), dconv.stride, dconv.padding, dconv.kh, dconv.kw,
                              fp8=_dg8(dAd8, dconv), sparse=sparse)
             conv_wgrad(dconv, dAd, x)
@@ -338,7 +330,7 @@ class BlockFn(torch.autograd.Function):
             # dx3 kept as (g, A, B, c): no apply pass (ops/bn_gram.py); when the next block's dgrad ran without x3,
             # sum(g xhat3) comes from T = g^T h2 (formed here, reused by the weight gradient)
             T = gram_T(dout, outs[-1], out=_gws(block, 0)) if getattr(block, "_bnb_nox", False) else None
-            dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None)
+            dA = gram_coef(bn_l, dout, T=T, w3=conv_l.w_bf16 if T is not None else None, hs=ctx.h2sum)
             dX = dout
         elif premasked:
             g8a = q.grad_out(a_last, bn_l) if (q is not None and fp8_dgrad_ok(conv_l)) else None
@@ -361,14 +353,13 @@ class BlockFn(torch.autograd.Function):
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 if isinstance(dA, GramBN):
                     dH = gram_dgrad(dA, conv, h_in, fz)
-                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1), P=ctx.gram_P)  # issued now: it reads dout, which conv1's dgrad
+                    g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1), P=ctx.gram_P,
+                                         bn=bn_l)  # issued now: it reads dout, which conv1's dgrad
                 else:                                    # accumulates into below
                     dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))
                 if h_in is None:  # xfuse: the weight gradient applies the BN on its operand staging
                     h_in = (acts[i - 1], xbn[i])
-                if not _DEFER_WGRAD and not isinstance(dA, GramBN):
-                    _wgrad(conv, dA, h_in)
                 dA_w = dA
                 if fz is not None:
                     g8a = q.grad_out(acts[i - 1], bn_prev) if (q is not None and fp8_dgrad_ok(pairs[i - 1][0])) else None
@@ -377,7 +368,7 @@ class BlockFn(torch.autograd.Function):
                 else:
                     dA, _ = bn_act_backward(dH, acts[i - 1], None, None, bn_prev, None, 0, True)
                     dA8 = None
-                if _DEFER_WGRAD and not isinstance(dA_w, GramBN):
+                if not isinstance(dA_w, GramBN):
                     # issued after the BN-backward pass: the side-stream weight gradient then runs
                     # beside the next (compute-bound) dgrad instead of the memory-bound BN pass
                     _wgrad(conv, dA_w, h_in)
@@ -397,10 +388,8 @@ class BlockFn(torch.autograd.Function):
                     torch.cuda.current_stream().wait_event(g_read)
                 igemm_dgrad(dA, conv.wt_bf16, (H, W), conv.stride, conv.padding, conv.kh, conv.kw, out=dX,
                             accumulate=True, bnb=fz, fp8=_dg8(dA8, conv), old_sub2=(ds is not None and sparse))
-                if _DEFER_WGRAD:  # issued by the previous block's backward after its BN pass
-                    streams.defer(lambda c=conv, g=dA, h=h_in: conv_wgrad(c, g, h))
-                else:
-                    conv_wgrad(conv, dA, h_in)
+                # issued by the previous block's backward after its BN pass
+                streams.defer(lambda c=conv, g=dA, h=h_in: conv_wgrad(c, g, h))
                 if fz is not None:
                     prev._bnb_done = True
                     prev._bnb_nox = nox

@@ -126,14 +126,17 @@ def bn_act_backward(dy: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor
 
 
 def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2,
-                      mode: int, g8=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                      mode: int, g8=None, slab_of=None, sgx_row: int = 0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Backward of act(bn(x) [+ res | + bn2(x2)]) for a gradient ``g`` that its
     producing dgrad already ReLU-masked and reduced into ``bn.work.scratch``
     (``ops.conv.BNBwdFuse``): one fold + one streaming apply pass.
     Returns (dx, dx2 | None); for mode 1 the residual-branch gradient is g.
     ``g8 = ((q, exp, amax) | None, (q2, exp2, amax2) | None)``: also write e5m2
-    copies of dx / dx2 for the fp8 dgrad (``Fp8State``)."""
+    copies of dx / dx2 for the fp8 dgrad (``Fp8State``).
+    ``slab_of`` / ``sgx_row`` (modes 0 / 1): the reductions sit in another BN's slab, sum(g xhat) in its row
+    ``sgx_row`` (a Gram-form bn3 whose dgrad epilogue also reduced the downsample BN: ops/block.py)."""
     w = bn.work
+    scratch = (slab_of if slab_of is not None else bn).work.scratch
     C = x.shape[-1]
     R = x.numel() // C
     dx = torch.empty_like(x)
@@ -141,9 +144,9 @@ def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tenso
     _lib.check(_lib.kernels().imk_bn_bwd_apply(
         g.data_ptr(), x.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(), _lib.ptr(x2),
         bn2.work.save.data_ptr() if mode == 2 else 0, bn2.weight.data_ptr() if mode == 2 else 0,
-        w.scratch.data_ptr(), dx.data_ptr(), _lib.ptr(dx2), bn.weight.grad.data_ptr(),
+        scratch.data_ptr(), dx.data_ptr(), _lib.ptr(dx2), bn.weight.grad.data_ptr(),
         bn.bias.grad.data_ptr(), bn2.weight.grad.data_ptr() if mode == 2 else 0,
-        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _g8desc(g8), _lib.stream_ptr()),
+        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _g8desc(g8), sgx_row, _lib.stream_ptr()),
         "bn bwd apply")
     notify_ready(bn.weight)
     notify_ready(bn.bias)

@@ -8,15 +8,18 @@ widest activation gradient of the block. Instead of writing it:
   per-channel (A, B, c) and accumulates dgamma / dbeta;
 * :func:`gram_dgrad` runs conv3's dgrad as ONE GEMM over the concatenated operand [g | h2] with the
   weights [diag(A) W3 | W3^T diag(B) W3] and the bias c W3, into bn2's fused backward epilogue;
-* :func:`gram_wgrad` forms conv3's weight gradient from g^T h2, the Gram matrix h2^T h2 and the
-  column sums of h2 (side stream), then one fix-up kernel.
+* :func:`gram_wgrad` forms conv3's weight gradient from g^T h2, the centred Gram matrix
+  h2^T h2 - s s^T / M and the column sums s of h2 (side stream), then one fix-up kernel.
+
+Every matrix that enters a variance or a mean-subtracted sum is centred before it is contracted with
+W3 (``gram_P``, the x-free ``gram_coef``), so a channel whose |mean| >> std keeps its variance
+(tests/test_bn_numerics_gpu.py).
 
 h2 (conv3's input, relu(bn2(x2))) has to exist: blocks that take this path keep it materialised
 in forward (``ops/block.py``)."""
 
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -27,12 +30,11 @@ from .grad_sink import notify_ready
 # split-K of the skinny Gram GEMMs (T = g^T h2, G = h2^T h2: a [4p][p] / [p][p] output over M ~ 1e5-3e6 pixels):
 # one wave of 512 blocks (2 per CU) on the v3 weight-gradient loop -- scripts/gram_bench.py at 1024 img, isolated:
 # G 128x128 90 -> 66 us, 256x256 74 -> 52, T 512x128 223 -> 187, 1024x256 186 -> 167 (the default 1024-block
-# target pays a second, partial wave). IMAGENT_GRAM_SPLITS=0: the default split (A/B).
-_GRAM_SPLITS = os.environ.get("IMAGENT_GRAM_SPLITS", "1") != "0"
+# target pays a second, partial wave).
 
 
 def _splits(co: int, ci: int) -> int:
-    if not _GRAM_SPLITS or co % 128 or ci % 128:  # (the register-staged kernel keeps its own choice)
+    if co % 128 or ci % 128:  # (the register-staged kernel keeps its own choice)
         return 0
     return max(16, 512 // ((co // 128) * (ci // 128)))
 
@@ -55,19 +57,21 @@ def gram_T(g: torch.Tensor, h2: torch.Tensor, out: torch.Tensor = None) -> torch
     return T
 
 
-def gram_coef(bn, g: torch.Tensor, T: torch.Tensor = None, w3: torch.Tensor = None) -> GramBN:
+def gram_coef(bn, g: torch.Tensor, T: torch.Tensor = None, w3: torch.Tensor = None,
+              hs: torch.Tensor = None) -> GramBN:
     """(A, B, c) of bn3 from its reduction slab; dgamma / dbeta accumulate as the apply pass would.
-    ``T`` (= g^T h2) and ``w3`` (conv3's bf16 weight [4p][p]): sum(g xhat) from them instead of the slab
-    (the producing dgrad ran without x, BNBwdFuse(None, ...): one read of x3 less)."""
+    ``T`` (= g^T h2), ``w3`` (conv3's bf16 weight [4p][p]) and ``hs`` (colsum(h2)): sum(g xhat) from them instead
+    of the slab, centred per element (the producing dgrad ran without x, BNBwdFuse(None, ...): one read of x3
+    less)."""
     w = bn.work
     C = bn.weight.shape[0]
     R = g.numel() // C
     coef = torch.empty((3, C), device=g.device, dtype=torch.float32)
     if T is not None:
         p = T.shape[1]
-        assert w3.numel() == C * p and w3.dtype == torch.bfloat16
+        assert w3.numel() == C * p and w3.dtype == torch.bfloat16 and hs is not None and hs.numel() == p
         _lib.check(_lib.kernels().imk_bn_bwd_coef_T(w.scratch.data_ptr(), T.data_ptr(), w3.data_ptr(),
-                                                    w.save.data_ptr(), bn.weight.data_ptr(),
+                                                    hs.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
                                                     bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
                                                     coef.data_ptr(), R, C, p, _lib.stream_ptr()), "bn bwd coef T")
     else:
@@ -77,6 +81,16 @@ def gram_coef(bn, g: torch.Tensor, T: torch.Tensor = None, w3: torch.Tensor = No
     notify_ready(bn.weight)
     notify_ready(bn.bias)
     return GramBN(g, coef, T)
+
+
+def gram_P(conv, G: torch.Tensor, s: torch.Tensor, rows: int) -> torch.Tensor:
+    """P = W3 (G - s s^T / rows) [4p][p] fp32: conv3's weight times the CENTRED Gram matrix of h2
+    (``bn_gram_gemm_kernel<0>``), on the current stream."""
+    C4, p = conv.out_channels, conv.in_channels
+    P = torch.empty((C4, p), device=G.device, dtype=torch.float32)
+    _lib.check(_lib.kernels().imk_bn_gram_p(conv.w_bf16.data_ptr(), G.data_ptr(), s.data_ptr(), P.data_ptr(), rows,
+                                            C4, p, _lib.stream_ptr()), "bn gram P")
+    return P
 
 
 def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tensor:
@@ -90,15 +104,10 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     bias = torch.empty((p,), device=h2.device, dtype=torch.float32)
     k = _lib.kernels()
     st = _lib.stream_ptr()
-    # Q = W3^T diag(B) W3 [p][p] (symmetric). hipBLASLt runs p = 128 as ONE 128 x 128 workgroup (36 us alone,
-    # 200-360 us in the step beside the weight-gradient stream): the own 16 x 16-tile kernel there (32 us in the
-    # step); p = 64 / 256 keep torch.mm (12-18 us in the step vs 15-23 / 54 us)
-    if p == 128:
-        Q = torch.empty((p, p), device=h2.device, dtype=torch.float32)
-        _lib.check(k.imk_bn_gram_q(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), p, C4, st), "gram Q")
-    else:
-        Wf = wt.view(p, C4).float()
-        Q = torch.mm(Wf * gb.coef[1], Wf.t())
+    # Q = W3^T diag(B) W3 [p][p] (symmetric), own fp32 kernel (hipBLASLt ran p = 128 as ONE 128 x 128 workgroup:
+    # 36 us alone, 200-360 us in the step beside the weight-gradient stream)
+    Q = torch.empty((p, p), device=h2.device, dtype=torch.float32)
+    _lib.check(k.imk_bn_gram_q(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), p, C4, st), "gram Q")
     _lib.check(k.imk_bn_gram_dgrad_weights(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), wcat.data_ptr(),
                                            bias.data_ptr(), p, C4, st), "gram dgrad weights")
     out = torch.empty((N, H, W, p), device=h2.device, dtype=torch.bfloat16)
@@ -114,29 +123,32 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     return out
 
 
-def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor):
+def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor, add_shift: torch.Tensor = None):
     """bn3's batch statistics without conv3's output (x3 = h2 W3^T): G = h2^T h2 into the zeroed ``G``, P =
-    W3 G, then mean = W3 s / M, E[x3^2] = rowsum(P * W3) / M (``bn_gram_fwd_stats_kernel``) into ``bn.work.stats``
-    / ``save``. Returns (aff [2][4p] = (gamma rstd, beta - mean gamma rstd) for conv3's epilogue, P; the weight
-    gradient reuses G and P)."""
+    W3 (G - s s^T / M) (centred), then mean = W3 s / M, var = rowsum(P * W3) / M (``bn_gram_fwd_stats_kernel``)
+    into ``bn.work.stats`` / ``save``. Returns (aff [2][4p] = (gamma rstd, beta - mean gamma rstd) for conv3's
+    epilogue, P; the weight gradient reuses P). ``add_shift`` [4p]: added to the returned shift (a downsample
+    block's shortcut-BN shift, folded into bn3's)."""
     C4, p = conv.out_channels, conv.in_channels
+    M = h2.numel() // p
     igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
-    P = torch.mm(conv.w_bf16.view(C4, p).float(), G)
+    P = gram_P(conv, G, s, M)
     aff = torch.empty((2, C4), device=h2.device, dtype=torch.float32)
     w = bn.work
     _lib.check(_lib.kernels().imk_bn_gram_fwd_stats(conv.w_bf16.data_ptr(), s.data_ptr(), P.data_ptr(),
                                                     bn.weight.data_ptr(), bn.bias.data_ptr(), w.stats.data_ptr(),
-                                                    w.save.data_ptr(), aff.data_ptr(), h2.numel() // p, C4, p,
+                                                    w.save.data_ptr(), aff.data_ptr(), _lib.ptr(add_shift), M, C4, p,
                                                     float(bn.eps), _lib.stream_ptr()), "bn gram fwd stats")
     return aff, P
 
 
 def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: torch.Tensor = None,
-               P: torch.Tensor = None):
-    """conv3.weight.grad += A (g^T h2) + B (W3 h2^T h2) + c colsum(h2), on the wgrad side stream.
+               P: torch.Tensor = None, bn=None):
+    """conv3.weight.grad += A (g^T h2) + B W3 Gc + (c + B mean) colsum(h2) (Gc = the centred Gram matrix of h2;
+    ``bn``: bn3, whose saved batch mean enters), on the wgrad side stream.
     ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``); ``G``: a zeroed
-    [p][p] fp32 accumulator (the per-step workspace) or None; ``P`` = W3 G when the forward already formed G
-    and P (``gram_fwd_stats``): then neither is recomputed.
+    [p][p] fp32 accumulator (the per-step workspace) or None; ``P`` = W3 Gc when the forward already formed it
+    (``gram_fwd_stats``): then neither G nor P is recomputed.
     Returns the side-stream event after the last read of ``g`` (or None without a side stream):
     the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
     side = streams.side_stream(h2.device) if h2.is_cuda else None
@@ -163,13 +175,13 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
         if own_s:
             colsum_into(h2.view(-1, p), s)
         if P is None:
-            P = torch.mm(conv.w_bf16.view(C4, p).float(), G)  # W3 G [4p][p]
+            P = gram_P(conv, G, s, h2.numel() // p)
         _lib.check(_lib.kernels().imk_bn_gram_wgrad_fixup(conv.weight.grad.data_ptr(), T.data_ptr(), P.data_ptr(),
-                                                          gb.coef.data_ptr(), s.data_ptr(), C4, p,
-                                                          _lib.stream_ptr()), "gram wgrad fixup")
+                                                          gb.coef.data_ptr(), bn.work.save.data_ptr(), s.data_ptr(),
+                                                          C4, p, _lib.stream_ptr()), "gram wgrad fixup")
         notify_ready(conv.weight)
     if side is not None:
-        streams.protect(*[t for t in (gb.g, gb.coef, h2, s, T, P) if t is not None])
+        streams.protect(*[t for t in (gb.g, gb.coef, h2, s, T, P, bn.work.save) if t is not None])
         streams.ensure_join_after_backward()
     return ev
 

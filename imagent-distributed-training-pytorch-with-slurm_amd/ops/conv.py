@@ -265,7 +265,7 @@ def igemm_dgrad(dy: torch.Tensor, wt: torch.Tensor, in_hw: Tuple[int, int], stri
         if sparse:
             assert S == 2 and KH == 1 and KW == 1 and pad == 0, "sparse: stride-2 1x1 dgrads only"
         else:
-            out.zero_()
+            _lib.zero_(out)
         skip_empty = True
     else:
         skip_empty = accumulate
@@ -422,11 +422,12 @@ def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tenso
 
 def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tensor] = None) -> None:
     gp = getattr(mod, "grad_pad", None)
-    if gp is not None:  # stem: [Co][KH][32] row-segment layout -> master [Co][KH][KW][Ci]
-        gp.zero_()
+    if gp is not None:  # stem: [Co][KH][32] row-segment layout (zero between steps) -> master [Co][Ci][KH][KW]
         igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw, stem=True)
-        real = gp[:, :, : mod.kw * 4].view(gp.shape[0], mod.kh, mod.kw, 4)[..., : mod.in_channels]
-        mod.weight.grad.permute(0, 2, 3, 1).add_(real)
+        g = mod.weight.grad
+        assert g.is_contiguous() and tuple(g.shape) == (gp.shape[0], mod.in_channels, mod.kh, mod.kw)
+        _lib.check(_lib.kernels().imk_stem_grad_fold(gp.data_ptr(), g.data_ptr(), gp.shape[0], mod.in_channels,
+                                                     mod.kh, mod.kw, _lib.stream_ptr()), "stem grad fold")
     else:
         igemm_wgrad(dy, x, mod.weight.grad, mod.stride, mod.padding, mod.kh, mod.kw, xbn=xbn)
     notify_ready(mod.weight)

@@ -91,6 +91,6 @@ class WeightQuantizer:
         self._n, self._max_n4, self.margin = len(weights), max_n4, margin
 
     def run(self) -> None:
-        self.amax.zero_()
+        _lib.zero_(self.amax)
         _lib.check(_lib.kernels().imk_quant_fp8_weights(self._descs.data_ptr(), self._n, self._max_n4,
                                                         self.margin, _lib.stream_ptr()), "fp8 weights")

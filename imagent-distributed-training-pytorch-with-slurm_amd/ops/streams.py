@@ -11,7 +11,7 @@ Dependencies that make this safe:
 * tensors read on the side stream are held (:func:`protect`) until the
   end-of-backward join, then released in main-stream order, so the caching
   allocator cannot recycle them while a side-stream kernel still reads them
-  (``IMAGENT_PROTECT=record`` uses ``record_stream`` instead);
+  (``record_stream`` instead measured the same img/s at 2.4x the reserved HBM);
 * the data-parallel reducer makes each bucket's all-reduce wait for the side
   stream as well as the main one (``parallel/ddp.py``), and the end of
   backward joins the side stream into the main one (the optimizer reads the
@@ -20,7 +20,6 @@ Dependencies that make this safe:
 
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional
 
 import torch
@@ -51,20 +50,9 @@ def side_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.St
 
 
 def _new_stream(idx: int):
-    """A torch pool stream, or (``IMAGENT_QUEUE_MODE=dedicated``) a full-CU-mask
-    HIP stream that the runtime puts on a hardware queue of its own
-    (``parallel/comm.py`` ``stream_mode``: measured slower), kept for the
-    process lifetime."""
-    from ..parallel.comm import stream_mode
-    if stream_mode() != 2:
-        return torch.cuda.Stream(device=idx)
-    import ctypes as C
-    from . import _lib
-    h = C.c_void_p()
-    rc = _lib.comm().imc_stream_create(idx, 2, C.byref(h))
-    if rc != 0:
-        raise RuntimeError(f"side stream: {_lib.comm().imc_last_error().decode()}")
-    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    """A torch pool stream (normal priority: the alternatives measured slower, ``parallel/comm.py``
+    :func:`stream_mode`), kept for the process lifetime."""
+    return torch.cuda.Stream(device=idx)
 
 
 def active_side_stream() -> Optional[torch.cuda.Stream]:
@@ -80,8 +68,7 @@ _keep: list = []
 # only once the allocator sees the side stream pass them, so with the CPU ahead
 # of the GPU every step got fresh blocks). Measured at R50 / 1024 img
 # (profiles/r50_b1024_allocator.md): reserved HBM 129 -> 52.7 GiB, peak 40.6 -> 45.9 GiB,
-# img/s unchanged. IMAGENT_PROTECT=record restores record_stream.
-_KEEP_EAGER = os.environ.get("IMAGENT_PROTECT", "keep") == "keep"
+# img/s unchanged.
 
 
 def protect(*tensors: torch.Tensor) -> None:
@@ -89,15 +76,10 @@ def protect(*tensors: torch.Tensor) -> None:
     reference is held until the side stream has been joined back into the
     main stream (default, and always while a HIP graph is being captured,
     where ``record_stream`` is not usable; the join is also the dependency
-    edge a captured graph needs). ``IMAGENT_PROTECT=record``: ``record_stream``."""
-    s = active_side_stream()
-    if s is None:
+    edge a captured graph needs)."""
+    if active_side_stream() is None:
         return
-    if _KEEP_EAGER or torch.cuda.is_current_stream_capturing():
-        _keep.extend(tensors)
-    else:
-        for t in tensors:
-            t.record_stream(s)
+    _keep.extend(tensors)
 
 
 def join_side_into_current() -> None:

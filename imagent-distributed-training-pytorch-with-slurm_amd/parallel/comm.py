@@ -65,20 +65,17 @@ class Communicator:
 
 
 def stream_mode() -> int:
-    """Kind of HIP stream for the comm stream (and the weight-gradient side
-    stream), ``IMAGENT_QUEUE_MODE``:
+    """Kind of HIP stream for the comm stream: plain, normal priority (0). The alternatives the native
+    library still implements measured slower on one MI355X at R50 / 1024 img with RCCL self collectives:
 
-    * ``plain`` (default): normal priority;
-    * ``priority``: highest-priority comm stream. Measured on one MI355X at
-      R50 / 1024 img with RCCL self collectives: 10.2k vs 12.1k img/s. The comm
-      stream spends the backward parked on barrier packets (waiting for the
-      next bucket's producers); while a high-priority queue holds work the
-      lower-priority queues' wave launches are throttled, and the main-stream
-      forward / BN kernels ran 10-40 % slower (stats_finalize 5x);
-    * ``dedicated``: full-CU-mask streams (a hardware queue each): 8.9k img/s.
+    * highest-priority comm stream (1): 10.2k vs 12.1k img/s. The comm stream spends the backward parked on
+      barrier packets (waiting for the next bucket's producers); while a high-priority queue holds work the
+      lower-priority queues' wave launches are throttled, and the main-stream forward / BN kernels ran
+      10-40 % slower (stats_finalize 5x);
+    * full-CU-mask streams (2, a hardware queue each): 8.9k img/s.
 
     Study: ``profiles/r50_b1024_comm_stream_study.md``."""
-    return {"dedicated": 2, "priority": 1, "plain": 0}[os.environ.get("IMAGENT_QUEUE_MODE", "plain")]
+    return 0
 
 
 class LocalCommunicator(Communicator):

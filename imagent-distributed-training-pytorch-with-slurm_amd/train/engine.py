@@ -90,6 +90,14 @@ class StepRunner:
                 return self.ddp(x)
         return self.ddp(x)
 
+    def _seed(self, loss, n: int):
+        key = (loss.device, loss.dtype, n)
+        cache = self.__dict__.setdefault("_seeds", {})
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.full((), 1.0 / n, device=loss.device, dtype=loss.dtype)
+        return t
+
     def train_step(self, micro) -> None:
         from ..ops import streams
         streams.reset()
@@ -100,7 +108,8 @@ class StepRunner:
                 ctx = self.ddp.no_sync() if i + 1 < n else _null()
                 with ctx:
                     loss = self.loss(self.forward(x), y)
-                    (loss / n if n > 1 else loss).backward()
+                    # the seed gradient 1 / n from a cached device scalar: no fill / div launch per step
+                    loss.backward(self._seed(loss, n))
         except BaseException:
             streams.reset()  # a failed backward may have left its join callback unrun
             self.ddp.abandon_backward()

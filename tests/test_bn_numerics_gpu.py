@@ -135,3 +135,74 @@ def test_deterministic_statistics():
     finally:
         cv.set_deterministic(prev)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+class _NS:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+@pytest.mark.parametrize("p", [128, 256])
+def test_gram_statistics_large_mean(p):
+    """bn3's statistics in the Gram form (ops/bn_gram.py gram_fwd_stats: x3 = h2 W3^T never formed) and on the
+    per-op path (conv epilogue, shifted sums) when |mean(x3)| / std(x3) >= 30: half of conv3's output channels
+    have weight rows aligned with the (positive, ReLU-like) mean of h2. Checked against fp64 statistics of
+    h2 W3^T over the same bf16 operands: mean to 1e-3 sd, variance to 1e-3 relative. Also the x-free backward
+    coefficient sum(g xhat3) (bn_bwd_coef_T_kernel: from T = g^T h2, centred per element) against fp64."""
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.bn import stats_finalize
+    from imagent_amd.ops.bn_gram import gram_T, gram_coef, gram_fwd_stats
+    from imagent_amd.ops.conv import colsum_into, igemm_fwd
+    torch.manual_seed(7)
+    N, H, C4 = 256, 32, 4 * p
+    M = N * H * H
+    h2 = (1.0 + 0.3 * torch.randn(N, H, H, p, device=DEV)).clamp_min(0).to(torch.bfloat16)
+    w = torch.randn(C4, p, device=DEV) / p ** 0.5
+    w[: C4 // 2] = (1.0 + 0.1 * torch.randn(C4 // 2, p, device=DEV)) / p  # aligned rows: mean ~1, std ~0.3/sqrt(p)
+    w3 = w.to(torch.bfloat16)
+    x3 = h2.reshape(M, p).double() @ w3.double().t()
+    mean64, var64 = x3.mean(0), x3.var(0, unbiased=False)
+    sd64 = var64.sqrt()
+    assert float((mean64[: C4 // 2].abs() / sd64[: C4 // 2]).min()) >= 30.0
+    bn = _NS(work=_work(C4), weight=torch.rand(C4, device=DEV) + 0.5, bias=torch.randn(C4, device=DEV) * 0.1,
+             eps=1e-5)
+    conv = _NS(out_channels=C4, in_channels=p, w_bf16=w3.view(C4, 1, 1, p))
+    s = torch.zeros(p, device=DEV)
+    colsum_into(h2.view(-1, p), s)
+    G = torch.zeros(p, p, device=DEV)
+    gram_fwd_stats(bn, conv, h2, s, G)
+    torch.cuda.synchronize()
+    mean, var = bn.work.stats[0].double(), bn.work.stats[1].double()
+    e_mean = float(((mean - mean64).abs() / sd64).max())
+    e_var = float(((var - var64).abs() / var64).max())
+    print(f"p={p}: Gram form mean err {e_mean:.2e} sd, var rel err {e_var:.2e}")
+    assert e_mean < 1e-3 and e_var < 1e-3
+    # per-op path: the conv epilogue's shifted sums over the stored bf16 x3 (second call: shift = first mean)
+    work = _work(C4)
+    for _ in range(2):
+        work.slab.zero_()
+        y = igemm_fwd(h2, conv.w_bf16, 1, 0, 1, 1, stats=work)
+        stats_finalize(work, M)
+        work.save[0].copy_(work.stats[0])
+    yd = y.double().reshape(-1, C4)
+    ym, yv = yd.mean(0), yd.var(0, unbiased=False)
+    pe_mean = float(((work.stats[0].double() - ym).abs() / yv.sqrt()).max())
+    pe_var = float(((work.stats[1].double() - yv).abs() / yv).max())
+    print(f"p={p}: per-op path mean err {pe_mean:.2e} sd, var rel err {pe_var:.2e}")
+    assert pe_mean < 1e-3 and pe_var < 1e-3
+    # x-free backward coefficient: g correlated with xhat3, nonzero mean (sum(g) ~ M / 2)
+    xhat = (x3 - mean64) / sd64
+    g = (0.5 + xhat + 0.5 * torch.randn_like(xhat)).float().to(torch.bfloat16)
+    bn.work.scratch.zero_()
+    S = _lib.STAT_SLOTS
+    bn.work.scratch[: S * 3 * C4].view(S, 3, C4)[0, 1].copy_(g.float().sum(0))  # slab row 1: sum(g)
+    bn.weight.grad = torch.zeros(C4, device=DEV)
+    bn.bias.grad = torch.zeros(C4, device=DEV)
+    bn.work.save.copy_(torch.stack([mean64.float(), (1.0 / sd64).float()]))
+    T = gram_T(g.view(N, H, H, C4), h2)
+    gram_coef(bn, g.view(N, H, H, C4), T=T, w3=w3, hs=s)
+    torch.cuda.synchronize()
+    ref = (g.double() * xhat).sum(0)
+    e_sgx = float(((bn.weight.grad.double() - ref).abs() / ref.abs()).max())
+    print(f"p={p}: x-free sum(g xhat) rel err {e_sgx:.2e}")
+    assert float(ref.abs().min()) > 0.1 * M and e_sgx < 1e-3

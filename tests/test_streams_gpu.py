@@ -1,9 +1,8 @@
-"""Weight-gradient side stream: operand lifetime modes vs no overlap.
+"""Weight-gradient side stream vs no overlap.
 
-Side-stream operands are either held until the end-of-backward join (default,
-``IMAGENT_PROTECT=keep``) or ``record_stream``'ed (``=record``). Both must give
-the update of a run with the side stream off, and the held list must be empty
-after every step (ops/streams.py; round-1 advice).
+Side-stream operands are held until the end-of-backward join (ops/streams.py
+``protect``). The run must give the update of a run with the side stream off,
+and the held list must be empty after every step (round-1 advice).
 
 Two steps from the same initial state and batches per mode (the second one
 exercises the steady state: buffers recycled from the first step); the
@@ -25,7 +24,7 @@ sys.path.insert(0, ROOT)
 DEV = torch.device("cuda:0")
 
 
-def _run(overlap, keep, monkeypatch):
+def _run(overlap):
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.models import resnet
     from imagent_amd.models.native import bind_native
@@ -35,7 +34,6 @@ def _run(overlap, keep, monkeypatch):
     from imagent_amd.train.engine import StepRunner
     from imagent_amd.train.meters import DeviceMetrics
     from imagent_amd.train.optim import FlatSGD
-    monkeypatch.setattr(streams, "_KEEP_EAGER", keep)
     torch.manual_seed(5)
     model = resnet.build("resnet18", num_classes=1000)
     order = list(reversed(range(len(list(model.parameters())))))
@@ -70,12 +68,11 @@ def _ratio(a, b):
     return (a * b).sum().item() / (b * b).sum().item()
 
 
-def test_protect_modes_match_no_overlap(monkeypatch):
-    ref = _run(False, True, monkeypatch)
-    for keep in (True, False):
-        got = _run(True, keep, monkeypatch)
-        for kind in (True, False):
-            r = _ratio(got[kind], ref[kind])
-            print(f"keep={keep} weights={kind}: projection ratio {r:.5f}")
-            assert abs(r - 1.0) < 0.1, (keep, kind, r)
-            assert got[kind].abs().max() > 0
+def test_side_stream_matches_no_overlap():
+    ref = _run(False)
+    got = _run(True)
+    for kind in (True, False):
+        r = _ratio(got[kind], ref[kind])
+        print(f"weights={kind}: projection ratio {r:.5f}")
+        assert abs(r - 1.0) < 0.1, (kind, r)
+        assert got[kind].abs().max() > 0
