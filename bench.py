@@ -244,6 +244,15 @@ def main(argv=None):
         t1 = time.perf_counter()
         coll_per_step = (comm.collectives - c0) / max(1, a.steps)
         T = max_over_ranks(t1 - t0)
+        # after the timed region: two more steps with the bucket timeline recorded (parallel/ddp.py CommTimeline:
+        # exposed communication after the last backward kernel, per-bucket issue offsets, comm-stream busy time)
+        overlap = None
+        if not a.graph:
+            ddp.comm_timeline(True)
+            steps(2)
+            sync()
+            overlap = ddp.timeline.stats()
+            ddp.comm_timeline(False)
         loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
         n_rccl = rccl_communicators()  # counted while the training communicator is open
         val = None
@@ -310,6 +319,7 @@ def main(argv=None):
                     "world_size": ctx.world_size,
                     "comm_nranks": getattr(comm, "nranks", comm.world_size),
                     "collectives_per_step": coll_per_step,
+                    "comm_overlap": overlap,
                     "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip" and not f32_hip,
                     "auto_batch_reduced": auto_reduced,
                     "bucket_mb": a.bucket_mb,

@@ -746,13 +746,13 @@ IMK_EXPORT int imk_xent_bwd(const float* logits, const int64_t* labels, const fl
 }
 
 // The stem's weight gradient from its row-segment layout gp [Co][KH][32] (channel-padded 4-channel pixels, kw * 4 +
-// ci) into the master gradient [Co][Ci][KH][KW] (+=, gradient accumulation), clearing gp for the next step's
-// atomic accumulation in the same pass (one launch instead of a fill + a strided add).
+// ci) into the master gradient, stored [Co][KH][KW][Ci] in the arena (+=, gradient accumulation), clearing gp for
+// the next step's atomic accumulation in the same pass (one launch instead of a fill + a strided add).
 __global__ __launch_bounds__(256) void stem_grad_fold_kernel(float* __restrict__ gp, float* __restrict__ grad, int Co,
                                                              int Ci, int KH, int KW) {
     const int n = Co * Ci * KH * KW;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
-        const int kw = e % KW, kh = (e / KW) % KH, ci = (e / (KW * KH)) % Ci, co = e / (KW * KH * Ci);
+        const int ci = e % Ci, kw = (e / Ci) % KW, kh = (e / (Ci * KW)) % KH, co = e / (Ci * KW * KH);
         float* src = gp + ((size_t)co * KH + kh) * 32 + kw * 4 + ci;
         grad[e] += *src;
         *src = 0.f;

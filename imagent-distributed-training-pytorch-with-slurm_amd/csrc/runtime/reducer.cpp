@@ -31,8 +31,12 @@ extern "C" {
 // Greedy size-capped bucketing over tensors in the given order.
 // The first bucket is capped at `first_cap` bytes, later ones at `cap`
 // (torch: kDefaultFirstBucketBytes = 1 MiB, kDefaultBucketBytesCap = 25 MiB).
-// A bucket is closed as soon as it reaches its cap. Returns #buckets.
-int32_t imr_plan_buckets(int32_t n, const int64_t* nbytes, int64_t first_cap, int64_t cap,
+// A bucket is closed as soon as it reaches its cap. `last_cap` > 0: the LAST
+// bucket is at most that many bytes (or one tensor): the trailing tensors are
+// split off the greedy last bucket -- it is the one all-reduce that cannot
+// overlap backward (issued after the last gradient), so it is kept small.
+// Returns #buckets.
+int32_t imr_plan_buckets(int32_t n, const int64_t* nbytes, int64_t first_cap, int64_t cap, int64_t last_cap,
                          int32_t* bucket_of) {
     if (n <= 0) return 0;
     int32_t b = 0;
@@ -45,6 +49,16 @@ int32_t imr_plan_buckets(int32_t n, const int64_t* nbytes, int64_t first_cap, in
             ++b;
             acc = 0;
             limit = cap;
+        }
+    }
+    if (last_cap > 0) {
+        int32_t start = n - 1;  // first tensor of the tail (at least the last tensor)
+        int64_t tail = nbytes[n - 1];
+        while (start > 0 && bucket_of[start - 1] == b && tail + nbytes[start - 1] <= last_cap)
+            tail += nbytes[--start];
+        if (start > 0 && bucket_of[start - 1] == b) {  // the greedy last bucket holds more: split it
+            ++b;
+            for (int32_t i = start; i < n; ++i) bucket_of[i] = b;
         }
     }
     return b + 1;

@@ -245,7 +245,7 @@ def _declare(name: str, lib) -> None:
         lib.imc_stream_create.argtypes = [i32, i32, C.POINTER(vp)]
         lib.imc_stream_destroy.argtypes = [vp]
     elif name == "runtime":
-        lib.imr_plan_buckets.argtypes = [i32, C.POINTER(C.c_int64), C.c_int64, C.c_int64,
+        lib.imr_plan_buckets.argtypes = [i32, C.POINTER(C.c_int64), C.c_int64, C.c_int64, C.c_int64,
                                          C.POINTER(C.c_int32)]
         lib.imr_plan_buckets.restype = i32
         lib.imr_tracker_new.argtypes = [i32, C.POINTER(C.c_int32), i32]

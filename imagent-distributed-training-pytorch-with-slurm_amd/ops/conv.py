@@ -422,10 +422,10 @@ def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tenso
 
 def _conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tensor] = None) -> None:
     gp = getattr(mod, "grad_pad", None)
-    if gp is not None:  # stem: [Co][KH][32] row-segment layout (zero between steps) -> master [Co][Ci][KH][KW]
+    if gp is not None:  # stem: [Co][KH][32] row-segment layout (zero between steps) -> master [Co][KH][KW][Ci]
         igemm_wgrad(dy, x, gp, mod.stride, mod.padding, mod.kh, mod.kw, stem=True)
-        g = mod.weight.grad
-        assert g.is_contiguous() and tuple(g.shape) == (gp.shape[0], mod.in_channels, mod.kh, mod.kw)
+        g = mod.weight.grad  # the arena's [Co][Ci][KH][KW] view of [Co][KH][KW][Ci] storage
+        assert tuple(g.shape) == (gp.shape[0], mod.in_channels, mod.kh, mod.kw) and g.permute(0, 2, 3, 1).is_contiguous()
         _lib.check(_lib.kernels().imk_stem_grad_fold(gp.data_ptr(), g.data_ptr(), gp.shape[0], mod.in_channels,
                                                      mod.kh, mod.kw, _lib.stream_ptr()), "stem grad fold")
     else:

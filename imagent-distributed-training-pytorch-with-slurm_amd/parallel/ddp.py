@@ -38,6 +38,7 @@ MI355X design:
 from __future__ import annotations
 
 import contextlib
+import time
 import zlib
 import ctypes as C
 from typing import Dict, List, Optional
@@ -52,8 +53,11 @@ from .comm import Communicator, LocalCommunicator
 MB = 1024 * 1024
 
 
-def plan_buckets(nbytes: List[int], first_cap: int, cap: int) -> List[int]:
-    """Bucket id per tensor (tensors given in bucket/layout order)."""
+def plan_buckets(nbytes: List[int], first_cap: int, cap: int, last_cap: int = 0) -> List[int]:
+    """Bucket id per tensor (tensors given in bucket/layout order): greedy, the first bucket capped at
+    ``first_cap`` bytes, the others at ``cap``; ``last_cap`` > 0 splits the trailing tensors (at most that many
+    bytes, at least one tensor) off the last bucket -- the all-reduce issued after the last gradient, which
+    nothing overlaps."""
     n = len(nbytes)
     if n == 0:
         return []
@@ -61,7 +65,7 @@ def plan_buckets(nbytes: List[int], first_cap: int, cap: int) -> List[int]:
         L = _lib.runtime()
         arr = (C.c_int64 * n)(*nbytes)
         out = (C.c_int32 * n)()
-        L.imr_plan_buckets(n, arr, first_cap, cap, out)
+        L.imr_plan_buckets(n, arr, first_cap, cap, last_cap, out)
         return list(out)
     except _lib.NativeLibraryMissing:
         ids, b, acc, lim = [], 0, 0, first_cap if first_cap > 0 else cap
@@ -70,6 +74,13 @@ def plan_buckets(nbytes: List[int], first_cap: int, cap: int) -> List[int]:
             acc += s
             if acc >= lim and i + 1 < n:
                 b, acc, lim = b + 1, 0, cap
+        if last_cap > 0:
+            start, tail = n - 1, nbytes[-1]
+            while start > 0 and ids[start - 1] == b and tail + nbytes[start - 1] <= last_cap:
+                start -= 1
+                tail += nbytes[start]
+            if start > 0 and ids[start - 1] == b:
+                ids[start:] = [b + 1] * (n - start)
         return ids
 
 
@@ -135,9 +146,92 @@ class _Tracker:
             self.h = None
 
 
+class CommTimeline:
+    """How one step's bucketed all-reduces overlap its backward (what an N-GPU run that disappoints needs
+    to say why; bench.py reports it as ``comm_overlap``).
+
+    On a GPU communicator with its own comm stream every mark is a timing event: ``begin`` on the compute
+    stream at the end of forward, per bucket ``issue`` on the comm stream once it has waited for the bucket's
+    producers (main AND weight-gradient side stream: the moment the all-reduce can start on the device) and
+    ``done`` after it, ``compute_end`` on the compute stream after the side stream joined (the last backward
+    kernel), ``joined`` after the compute stream waited for the comm stream. Without device events (gloo / CPU)
+    the marks are host clock readings at the same program points.
+
+    ``stats()`` (synchronises): ``exposed_comm_ms`` = compute_end -> joined (communication the optimizer waits
+    for after the last backward kernel), ``comm_stream_busy_ms`` = sum over buckets of issue -> done (device
+    only), ``bucket_issue_ms`` / ``bucket_done_ms`` relative to ``begin``, ``backward_ms`` = begin ->
+    compute_end, ``issue_order`` = bucket ids in issue order."""
+
+    def __init__(self, ddp: "DataParallel"):
+        self.ddp = ddp
+        s = getattr(ddp.comm, "stream", None)
+        self.dev = s is not None and ddp.arena.G.is_cuda and torch.cuda.is_available()
+        self.stream = s
+        self._reset()
+
+    def _reset(self):
+        self.t0 = self.tc = self.tj = None
+        self.iss, self.dn, self.order = {}, {}, []
+
+    def _mark(self, stream=None):
+        if not self.dev:
+            return time.perf_counter()
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream if stream is not None else torch.cuda.current_stream())
+        return e
+
+    def begin(self):
+        self._reset()
+        self.t0 = self._mark()
+
+    def issue(self, b: int):
+        if self.t0 is None:
+            return
+        if self.dev:  # the comm stream waits for the bucket's producers first: the event marks the device start
+            self.ddp.comm.depend_on(torch.cuda.current_stream())
+        self.iss[b] = self._mark(self.stream)
+        self.order.append(b)
+
+    def done(self, b: int):
+        if self.t0 is not None:
+            self.dn[b] = self._mark(self.stream)
+
+    def compute_end(self):
+        if self.t0 is not None:
+            self.tc = self._mark()
+
+    def joined(self):
+        if self.t0 is not None:
+            self.tj = self._mark()
+
+    def _ms(self, a, b) -> float:
+        if self.dev:
+            return float(a.elapsed_time(b))
+        return 1000.0 * (b - a)
+
+    def stats(self) -> dict:
+        if self.t0 is None or self.tj is None:
+            return {}
+        if self.dev:
+            torch.cuda.synchronize()
+        nb = len(self.ddp.buckets)
+        out = {
+            "exposed_comm_ms": round(self._ms(self.tc, self.tj), 3),
+            "backward_ms": round(self._ms(self.t0, self.tc), 3),
+            "bucket_issue_ms": [round(self._ms(self.t0, self.iss[b]), 3) if b in self.iss else None for b in range(nb)],
+            "bucket_done_ms": ([round(self._ms(self.t0, self.dn[b]), 3) if b in self.dn else None for b in range(nb)]
+                               if self.dev else None),
+            "comm_stream_busy_ms": (round(sum(self._ms(self.iss[b], self.dn[b]) for b in self.iss if b in self.dn), 3)
+                                    if self.dev else None),
+            "issue_order": list(self.order),
+            "clock": "device events" if self.dev else "host",
+        }
+        return out
+
+
 class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, arena: ParamArena, comm: Optional[Communicator] = None,
-                 bucket_cap_mb: float = 16.0, first_bucket_mb: float = 2.0,
+                 bucket_cap_mb: float = 16.0, first_bucket_mb: float = 2.0, last_bucket_mb: float = 1.0,
                  broadcast_buffers: str = "eval", rebuild_buckets: bool = True,
                  find_unused_parameters: bool = False, use_autograd_hooks: Optional[bool] = None,
                  probe_order: bool = False, grad_reduce_dtype: str = "fp32"):
@@ -147,6 +241,10 @@ class DataParallel(nn.Module):
         self.comm = comm or LocalCommunicator()
         self.cap = int(bucket_cap_mb * MB)
         self.first_cap = int(first_bucket_mb * MB)
+        self.last_cap = int(last_bucket_mb * MB)
+        # per-step record of how the bucket all-reduces overlap backward (comm_timeline(), bench JSON); off
+        # unless asked for: a few event records per bucket
+        self.timeline: Optional["CommTimeline"] = None
         self.broadcast_buffers = broadcast_buffers
         self.rebuild_pending = rebuild_buckets
         self.find_unused = find_unused_parameters
@@ -198,7 +296,7 @@ class DataParallel(nn.Module):
     def _plan(self):
         order = self.arena.order
         nbytes = [self.arena.nbytes_of(i) for i in order]
-        bid_in_order = plan_buckets(nbytes, self.first_cap, self.cap)
+        bid_in_order = plan_buckets(nbytes, self.first_cap, self.cap, self.last_cap)
         nb = (max(bid_in_order) + 1) if bid_in_order else 0
         bucket_of = [0] * len(order)
         for pos, i in enumerate(order):
@@ -264,7 +362,14 @@ class DataParallel(nn.Module):
     def forward(self, *args, **kw):
         if self.broadcast_buffers == "always" and self.module.training:
             self.sync_buffers()
-        return self.module(*args, **kw)
+        out = self.module(*args, **kw)
+        if self.timeline is not None and self.module.training and torch.is_grad_enabled():
+            self.timeline.begin()  # end of forward ~ start of backward (the loss kernel is microseconds)
+        return out
+
+    def comm_timeline(self, on: bool = True) -> None:
+        """Record the next steps' bucket timing (:class:`CommTimeline`); read it with ``timeline.stats()``."""
+        self.timeline = CommTimeline(self) if on else None
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -295,10 +400,15 @@ class DataParallel(nn.Module):
             # bucket members may have been produced on the wgrad side stream:
             # the all-reduce waits for it too (main stream not blocked)
             self.comm.depend_on(side)
+        tl = self.timeline
+        if tl is not None:
+            tl.issue(b)
         if self._g16 is None:
             self.comm.allreduce_(self.arena.G[lo:hi], "avg")
         else:
             self._launch_bf16(b, lo, hi)
+        if tl is not None:
+            tl.done(b)
         if self.probe_order:
             self._probe(b, lo, hi)
 
@@ -368,7 +478,11 @@ class DataParallel(nn.Module):
             for b in range(len(self.buckets) - missing, len(self.buckets)):
                 self._launch(b)
         streams.join_side_into_current()  # the optimizer reads the gradient arena
+        if self.timeline is not None:
+            self.timeline.compute_end()
         self.comm.join()
+        if self.timeline is not None:
+            self.timeline.joined()
         for b in self._g16_pending:
             lo, hi, _ = self.buckets[b]
             self.arena.G[lo:hi].copy_(self._g16[lo:hi])

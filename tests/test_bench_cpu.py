@@ -31,3 +31,7 @@ def test_bench_self_launches_two_ranks(tmp_path):
     assert out["config"]["collectives_per_step"] >= 1
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert out["dtype"] == "fp32"  # the CPU torch path does not autocast: say so
+    ov = out["config"]["comm_overlap"]  # bucket timeline of a step after the timed region (parallel/ddp.py)
+    nb = len(out["config"]["bucket_plan_mb"])
+    assert ov["issue_order"] == list(range(nb)) and len(ov["bucket_issue_ms"]) == nb
+    assert ov["exposed_comm_ms"] >= 0 and ov["backward_ms"] > 0

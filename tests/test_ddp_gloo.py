@@ -139,3 +139,60 @@ def test_bf16_gradient_allreduce_tracks_fp32():
         assert abs(a - b) <= 0.05 + 0.05 * abs(a), (i, a, b)
     assert rows[-1][0] < 0.5 * rows[0][0] and rows[-1][1] < 0.5 * rows[0][1], (rows[0], rows[-1])
     assert any(a != b for a, b in rows[1:]), "bf16 path took no effect"
+
+
+def _timeline_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import json
+    from imagent_amd.models import resnet
+    from imagent_amd.models.arena import ParamArena
+    from imagent_amd.parallel.comm import TorchCommunicator
+    from imagent_amd.parallel.ddp import DataParallel
+    from imagent_amd.train.optim import FlatSGD
+
+    torch.manual_seed(3)
+    model = resnet.resnet18(num_classes=10)
+    order = list(reversed(range(len(list(model.parameters())))))  # the backward's ready order
+    arena = ParamArena(list(model.named_parameters()), "cpu", order=order)
+    ddp = DataParallel(model, arena, TorchCommunicator(), bucket_cap_mb=4.0, first_bucket_mb=0.5,
+                       rebuild_buckets=False)
+    opt = FlatSGD(arena, lr=0.01, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(rank)
+    stats = []
+    for step in range(2):
+        ddp.comm_timeline(step == 1)
+        x = torch.randn(4, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        opt.zero_grad()
+        F.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        if ddp.timeline is not None:
+            stats.append(ddp.timeline.stats())
+    with open(os.path.join(outdir, f"t{rank}.json"), "w") as f:
+        json.dump({"stats": stats[-1], "sizes_mb": ddp.bucket_sizes_mb()}, f)
+    dist.destroy_process_group()
+
+
+def test_comm_timeline_two_ranks():
+    """CommTimeline (the bench JSON's comm_overlap) on 2 gloo ranks: every bucket is issued exactly once, in
+    plan order, at non-decreasing offsets from the end of forward; the last bucket -- the one all-reduce issued
+    after the last gradient, which nothing overlaps -- is at most 1 MiB (the planner's last_cap); the exposed
+    time after the last backward kernel is reported."""
+    import json
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_timeline_worker, args=(world, _free_port(), d), nprocs=world, start_method="spawn",
+                           join=True)
+        for r in range(world):
+            out = json.load(open(os.path.join(d, f"t{r}.json")))
+            st, sizes = out["stats"], out["sizes_mb"]
+            nb = len(sizes)
+            assert nb > 2
+            assert st["issue_order"] == list(range(nb)), st["issue_order"]
+            iss = st["bucket_issue_ms"]
+            assert all(v is not None and v >= 0 for v in iss) and iss == sorted(iss), iss
+            assert sizes[-1] <= 1.0, sizes
+            assert st["exposed_comm_ms"] >= 0 and st["backward_ms"] > 0 and st["clock"] == "host"
