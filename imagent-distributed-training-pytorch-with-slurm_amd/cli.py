@@ -49,8 +49,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--num-classes", type=int, default=1000, help="synthetic data only")
     p.add_argument("--synthetic-train-size", type=int, default=1281167)
     p.add_argument("--synthetic-val-size", type=int, default=50000)
-    p.add_argument("--synthetic-task", default="random", choices=["random", "colour"],
-                   help="random: uniform noise + labels (throughput); colour: learnable class-coloured images")
+    p.add_argument("--synthetic-task", default="random", choices=["random", "colour", "mix"],
+                   help="random: uniform noise + labels (throughput); colour: learnable class-coloured images; "
+                        "mix: overlapping class Gaussians over smooth random bases (Bayes top-1 ~85 %% at 100 classes)")
     p.add_argument("--flip", action="store_true", help="random horizontal flip (reference: none)")
     # --- optimisation ---
     p.add_argument("--optimizer", default="sgd",

@@ -433,6 +433,22 @@ __device__ __forceinline__ void epilogue(const IGemmArgs& a, const f32x4 (&acc)[
 // loaded into registers at kernel START (epi_prefetch), so their HBM latency hides under the main loop instead
 // of stalling the epilogue after it (v3; the short-K dgrads are epilogue-bound: 1024@14 -> 256 dgrad 251 us,
 // with the fused BN backward 443 us before this)
+// Staged-epilogue LDS swizzle (epilogue_lds_put): byte b of tile row r sits at b ^ ((r & 15) << 3) -- the row's
+// 8-B slots XORed with the row's low 4 bits; shared with the streaming kernel's per-wave epilogue (conv_stream.hip).
+__host__ __device__ constexpr int epi_swz(int row, int byte) { return byte ^ ((row & 15) << 3); }
+
+// the 16-B chunk cc of a swizzled row r: chunk cc ^ ((r >> 1) & 7), its two 8-B halves swapped when r is odd
+__device__ __forceinline__ u32x4 epi_read(const char* base, int row, int pitch, int cc) {
+    const u32x4 t = *reinterpret_cast<const u32x4*>(base + row * pitch + ((cc * 16) ^ ((row & 14) << 3)));
+    return (row & 1) ? u32x4{t[2], t[3], t[0], t[1]} : t;
+}
+
+// per-(quantity, channel-in-chunk) block stride of the statistics fold image [nq][8][RG][CPR] (floats): padded so
+// the cc-fastest reads of two (or four) consecutive blocks fall in distinct banks
+__host__ __device__ constexpr int epi_red_stride(int BN, int NT) {
+    return (NT / (BN / 8)) * (BN / 8) + ((BN / 8) < 32 ? (BN / 8) : 0);
+}
+
 template <int BM, int BN, int NT>
 struct EpiPF {
     static constexpr int CPR = BN / 8, RG = NT / CPR, NQ = BM / RG;
@@ -466,7 +482,13 @@ __device__ __forceinline__ void epi_prefetch(const IGemmArgs& a, EpiPF<BM, BN, N
 template <int BM, int BN, int NT, class Put>
 __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, char* smem, int m0, int n0, int tid,
                                                  float* st, const EpiPF<BM, BN, NT>* pf = nullptr) {
-    constexpr int P = BN * 2 + 16;  // LDS row pitch, bytes
+    // LDS image of the bf16 tile: row pitch P = BN * 2 bytes (a multiple of the 256-B bank row for BN >= 128) with
+    // the 8-B slots XOR-swizzled by the row: slot s of row r at s ^ (r & 15) (epi_swz). The fragment writes
+    // (ds_write_b64, 16 lanes = 16 consecutive rows, one column) then cover 16 distinct slots of a 128-B bank window
+    // and the row-chunk reads (ds_read_b128: a 16-B chunk cc of row r sits at chunk cc ^ ((r >> 1) & 7), halves
+    // swapped when r is odd) hit 16 distinct 16-B slots per lane group: conflict-free both ways (the padded
+    // BN * 2 + 16 pitch it replaces had 2-way conflicts on both)
+    constexpr int P = BN * 2;       // LDS row pitch, bytes
     constexpr int CPR = BN / 8;     // 16-B chunks per row
     constexpr int RG = NT / CPR;    // rows processed concurrently (row groups)
     constexpr int NQ = BM / RG;     // chunks per thread
@@ -599,7 +621,7 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
         for (int u = 0; u < QB; ++u) {
             if (e[u] < 0) continue;
             const int row = rg + RG * (q0 + u);
-            const u32x4 t = *reinterpret_cast<const u32x4*>(smem + row * P + cc * 16);
+            const u32x4 t = epi_read(smem, row, P, cc);
             float v[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -666,23 +688,27 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
         }
     }
     if (!st) return;
-    // (3) fold the RG row groups per channel in LDS, one atomic per channel and quantity
+    // (3) fold the RG row groups per channel in LDS, one atomic per channel and quantity. Image [nq][8][RG][CPR]
+    // (+ pad per (q, c) block): the writes (fixed q, c; 32 lanes = consecutive (rg, cc)) and the reads (cc fastest)
+    // are conflict-free ([nq][RG][BN] had 8-way conflicts on the writes)
     const int nq = has_x2 ? 3 : 2;
-    float* red = reinterpret_cast<float*>(smem);  // [nq][RG][BN]
+    constexpr int RS = epi_red_stride(BN, NT);
+    float* red = reinterpret_cast<float*>(smem);
     __syncthreads();  // everyone is done reading the tile
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        red[(0 * RG + rg) * BN + cc * 8 + c] = s1[c];
-        red[(1 * RG + rg) * BN + cc * 8 + c] = s2[c];
-        if (has_x2) red[(2 * RG + rg) * BN + cc * 8 + c] = s3[c];
+        red[(0 * 8 + c) * RS + rg * CPR + cc] = s1[c];
+        red[(1 * 8 + c) * RS + rg * CPR + cc] = s2[c];
+        if (has_x2) red[(2 * 8 + c) * RS + rg * CPR + cc] = s3[c];
     }
     __syncthreads();
     for (int idx = tid; idx < nq * BN; idx += NT) {
-        const int qi = idx / BN, ch = idx - qi * BN;
+        const int qi = idx / BN, r = idx - qi * BN;
+        const int c8 = r / CPR, k = r - c8 * CPR, ch = k * 8 + c8;
         if (n0 + ch >= a.Nout) continue;
         float sum = 0.f;
 #pragma unroll 8
-        for (int g = 0; g < RG; ++g) sum += red[(qi * RG + g) * BN + ch];
+        for (int g = 0; g < RG; ++g) sum += red[(qi * 8 + c8) * RS + g * CPR + k];
         atomicAdd(st + qi * a.Nout + n0 + ch, sum);
     }
 }
@@ -699,7 +725,8 @@ __device__ __forceinline__ void epilogue_lds(const IGemmArgs& a, const f32x4 (&a
             for (int i = 0; i < FN; ++i) {
                 const int row = wrow0 + j * 16 + (lane & 15), col = wcol0 + i * 16 + (lane >> 4) * 4;
                 const f32x4 v = acc[i][j];
-                *reinterpret_cast<u32x2*>(sm + row * P + col * 2) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+                *reinterpret_cast<u32x2*>(sm + row * P + epi_swz(row, col * 2)) =
+                    u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
             }
     };
     epilogue_lds_put<BM, BN, NT>(a, put, smem, m0, n0, tid, st, pf);
@@ -1137,8 +1164,8 @@ int resident_blocks(KernelT kern, size_t lds, int threads = 256) {
 
 // LDS bytes the staged epilogue needs: the bf16 tile, then the statistics fold
 inline size_t epi_lds_bytes(int BM, int BN, int NT) {
-    const size_t tile = (size_t)BM * (BN * 2 + 16);
-    const size_t red = (size_t)3 * (NT / (BN / 8)) * BN * sizeof(float);
+    const size_t tile = (size_t)BM * BN * 2;
+    const size_t red = (size_t)3 * 8 * epi_red_stride(BN, NT) * sizeof(float);
     return std::max(tile, red);
 }
 

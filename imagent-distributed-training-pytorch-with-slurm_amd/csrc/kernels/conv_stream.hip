@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     constexpr int RP = stream_rp<STEM, K + K2>();   // LDS weight row pitch, chunks
     constexpr int RB = RP * 16;                     // ... bytes
     constexpr int SWM = (RP < 16 ? RP : 16) - 1;    // chunk swizzle mask: conflict-free A reads
-    constexpr int EP = BN * 2 + 16;   // epilogue LDS row pitch (bytes)
+    constexpr int EP = BN * 2;        // epilogue LDS row pitch (bytes), rows swizzled as the staged epilogue (epi_swz)
     constexpr int CH = BN / 8;        // 16-B output chunks per pixel
     constexpr int PPR = 64 / CH;      // pixels per epilogue read instruction
     constexpr int NR = 16 / PPR;      // epilogue reads per 16-pixel group
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             // results were consumed) before these writes land.
 #pragma unroll
             for (int i = 0; i < FN; ++i)
-                *reinterpret_cast<u32x2*>(sE + fr * EP + (i * 16 + fq * 4) * 2) =
+                *reinterpret_cast<u32x2*>(sE + fr * EP + epi_swz(fr, (i * 16 + fq * 4) * 2)) =
                     u32x2{pack_bf2(acc[i][0], acc[i][1]), pack_bf2(acc[i][2], acc[i][3])};
             __builtin_amdgcn_wave_barrier();
             // (2) coalesced row chunks: pixel q*PPR + lane/CH, channels n .. n+7
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 for (int u = 0; u < QB; ++u) {
                     const int q = q0 + u;
                     const int p = q * PPR + lane / CH;
-                    const u32x4 t = *reinterpret_cast<const u32x4*>(sE + p * EP + cc * 16);
+                    const u32x4 t = epi_read(sE, p, EP, cc);
                     if (e[q] < 0) continue;
                     float v[8];
 #pragma unroll
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
 template <int K, int BN, int D, int MODE, bool STEM = false, bool XBN = false, int K2 = 0>
 int launch_stream1(const IGemmArgs& a, hipStream_t st) {
     constexpr int RP = stream_rp<STEM, K + K2>();
-    const size_t lds = (size_t)BN * RP * 16 + 4 * 16 * (BN * 2 + 16);
+    const size_t lds = (size_t)BN * RP * 16 + 4 * 16 * (BN * 2);
     static int resident = 0;
     if (resident == 0) resident = resident_blocks(conv_stream_kernel<K, BN, D, MODE, STEM, XBN, K2>, lds);
     const int nsl = a.Nout / BN;

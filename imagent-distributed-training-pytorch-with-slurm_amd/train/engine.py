@@ -232,13 +232,17 @@ class Trainer:
         if a.data == "synthetic":
             self.num_classes = a.num_classes
             task = getattr(a, "synthetic_task", "random")
-            pool = 4 if task == "random" else 16
+            # mix: every training batch distinct (the accuracy must come from generalising, not recall)
+            pool = 4 if task == "random" else 16 if task == "colour" else None
+            if pool is None:
+                pool = max(1, min(a.synthetic_train_size // a.batch_size, 4096))
             self.train_src = SyntheticImageNet(a.synthetic_train_size, a.image_size, a.num_classes,
                                                a.batch_size, self.device, a.seed, rank=rk, task=task,
                                                pool_batches=pool)
             self.val_src = SyntheticImageNet(a.synthetic_val_size, a.image_size, a.num_classes,
                                              a.batch_size, self.device, a.seed + 1, rank=rk, task=task,
-                                             pool_batches=pool)
+                                             pool_batches=pool if task != "mix" else
+                                             max(1, a.synthetic_val_size // a.batch_size))
             self.n_train, self.n_val = a.synthetic_train_size, a.synthetic_val_size
             self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=a.seed)
             self.val_sampler = ShardSampler(self.n_val, ws, rk, shuffle=True, seed=a.seed)

@@ -56,6 +56,15 @@ def main():
                          torch.zeros(nbw * C, device=dev))
         return bn
 
+    # achievable streaming rate on this box: a 2-stream copy and a 3-stream add of the layer-1 activation size
+    ra = torch.randn(B, 56, 56, 64, device=dev).to(torch.bfloat16)
+    rb, rc = torch.randn_like(ra), torch.empty_like(ra)
+    nb0 = ra.numel() * 2
+    tc = timeit(lambda: rc.copy_(ra))
+    tadd = timeit(lambda: torch.add(ra, rb, out=rc))
+    print(f"reference: copy {nb0 * 2 / tc / 1e6:.2f} TB/s, add (2 in, 1 out) {nb0 * 3 / tadd / 1e6:.2f} TB/s "
+          f"({nb0 / 1e6:.0f} MB per tensor)")
+    del ra, rb, rc
     tot_f = tot_b = tot_rf = tot_rb = 0.0
     print(f"{'C':>5} {'H':>4} mode cnt | {'fwd us':>8} {'TB/s':>5} | {'bwd us':>8} {'TB/s':>5}")
     for C, H, mode, cnt in sites:
