@@ -77,8 +77,10 @@ __global__ __launch_bounds__(256) void bn_gram_dgrad_weights_kernel(const bf16_t
 
 // The small fp32 GEMMs of the Gram form, C[M][N] = sum_k A(m, k) B(k, n), on the VALU (fp32 products: P feeds
 // bn3's variance, which must not lose what the centring keeps). 64 x 64 output tile per block, 4 x 4 per thread,
-// K staged through LDS in chunks of 16 ([k][m] / [k][n] images read as float4). No split-K, no atomics: the
-// grids are small (16 - 64 blocks at R50) and run beside the weight-gradient stream. M, N % 64 == 0, K % 16 == 0.
+// K staged through LDS in chunks of 16 ([k][m] / [k][n] images read as float4), split over gridDim.z blocks of 64 k
+// each (~256 blocks at R50: the unsplit 16-64-block grids waited out one global round trip per chunk, 65 us per
+// p = 256 Q in the step) that ADD into the zeroed output (fp32 atomics; the per-step zeroed Gram workspace).
+// M, N % 64 == 0, K % 64 == 0.
 //  MODE 0: P = W3 Gc, the centred Gram matrix Gc = G - s s^T / rows formed on the operand load
 //          (A(o, j) = W3[o][j], bf16 [C4][p]; B(j, i) = G[j][i] - s[j] s[i] / rows; M = C4, N = K = p);
 //  MODE 1: Q = W3^T diag(B) W3 for the folded dgrad weights (A(i, o) = wt[i][o] B_o, B(o, j) = wt[j][o],
@@ -98,7 +100,8 @@ __global__ __launch_bounds__(256) void bn_gram_gemm_kernel(const bf16_t* __restr
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-    for (int k0 = 0; k0 < K; k0 += 16) {
+    const int kb = blockIdx.z * 64;
+    for (int k0 = kb; k0 < kb + 64; k0 += 16) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {  // A: 64 rows x 16 k, k fastest in memory
             const int e = tid + 256 * q, r = e >> 4, kk = e & 15;
@@ -132,8 +135,8 @@ __global__ __launch_bounds__(256) void bn_gram_gemm_kernel(const bf16_t* __restr
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<f32x4*>(out + (size_t)(m0 + ty * 4 + i) * N + n0 + tx * 4) =
-            f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(out + (size_t)(m0 + ty * 4 + i) * N + n0 + tx * 4 + j, acc[i][j]);
 }
 
 // dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + (c_o + B_o mean_o) s[i]   (T = g^T h2, P = W3 Gc with the centred
@@ -259,20 +262,20 @@ IMK_EXPORT int imk_bn_gram_dgrad_weights(const void* wt, int ldw, const float* c
     return 0;
 }
 
-// Q = W3^T diag(B) W3 [p][p] (wt = W3^T [p][ldw] bf16)
+// Q += W3^T diag(B) W3 [p][p] (wt = W3^T [p][ldw] bf16; Q zeroed by the caller)
 IMK_EXPORT int imk_bn_gram_q(const void* wt, int ldw, const float* coef, float* Q, int p, int C4, void* stream) {
-    if (p <= 0 || p % 64 || C4 <= 0 || C4 % 16 || ldw < C4) return -100;
-    hipLaunchKernelGGL(bn_gram_gemm_kernel<1>, dim3(p / 64, p / 64), dim3(256), 0, (hipStream_t)stream,
+    if (p <= 0 || p % 64 || C4 <= 0 || C4 % 64 || ldw < C4) return -100;
+    hipLaunchKernelGGL(bn_gram_gemm_kernel<1>, dim3(p / 64, p / 64, C4 / 64), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)wt, ldw, nullptr, nullptr, coef, Q, p, p, C4, 0.f);
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
-// P = W3 (G - s s^T / rows) [C4][p] (W3 [C4][p] bf16, G [p][p], s [p])
+// P += W3 (G - s s^T / rows) [C4][p] (W3 [C4][p] bf16, G [p][p], s [p]; P zeroed by the caller)
 IMK_EXPORT int imk_bn_gram_p(const void* w, const float* G, const float* s, float* P, long rows, int C4, int p,
                              void* stream) {
     if (rows <= 0 || p <= 0 || p % 64 || C4 <= 0 || C4 % 64) return -100;
-    hipLaunchKernelGGL(bn_gram_gemm_kernel<0>, dim3(p / 64, C4 / 64), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(bn_gram_gemm_kernel<0>, dim3(p / 64, C4 / 64, p / 64), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)w, p, G, s, nullptr, P, C4, p, p, 1.f / (float)rows);
     IMK_CHECK_LAUNCH();
     return 0;

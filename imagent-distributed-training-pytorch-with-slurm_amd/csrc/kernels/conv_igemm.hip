@@ -155,9 +155,14 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
-    if (tile == 17 || tile == 18) {  // v3 main loop (conv_igemm_v3.h)
+    if (tile == 17 || tile == 18 || tile == 27 || tile == 28) {  // v3 main loop (conv_igemm_v3.h); 27 / 28: tap-inner
         if (!use_lds || !v3_ok(a)) return -105;
-        return tile == 17 ? launch_v3<256, 256, 2, 2, 8, 128>(a, st) : launch_v3<128, 128, 2, 2, 4, 128>(a, st);
+        switch (tile) {
+            case 17: return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+            case 18: return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
+            case 27: return launch_v3<256, 256, 2, 2, 8, 128, 2, 0, true>(a, st);
+            default: return launch_v3<128, 128, 2, 2, 4, 128, 2, 0, true>(a, st);
+        }
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);

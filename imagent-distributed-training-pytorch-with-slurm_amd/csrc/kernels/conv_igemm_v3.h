@@ -53,7 +53,12 @@ __device__ __forceinline__ void v3_dma(__amdgpu_buffer_rsrc_t r, char* lds, uint
 // reads its 8 k (32 B, chunks 2g, 2g + 1 as fp8) and splits them into bf16 hi + lo in registers; x w =
 // hi hi + hi lo + lo hi on three v_mfma_f32_16x16x32_bf16 (fp32 accumulate, ~2^-16 relative per product);
 // direct fp32 epilogue (+ bias, + accumulate).
-template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0>
+// TI: K order of a multi-tap conv. false (default): filter tap outer, channel slice inner (consecutive stages read
+// consecutive 128-B chunks of the same pixel rows). true (A/B, explicit tiles 27 / 28): channel slice outer, tap
+// inner -- the 9 taps of a 3x3 re-read nearly the same rows of one 128-B channel column in 9 consecutive stages,
+// a smaller L2 working set per tile; measured SLOWER in the R50 step (v3 128x128 14.6 -> 17.3 ms/step, 256x256
+// 6.9 -> 8.0, round 5): the tap order's row locality is worth more than the smaller window.
+template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0, bool TI = false>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(const IGemmArgs a) {
     constexpr int WM = NW / WN;
     constexpr int TM = BM / WM, TN = BN / WN;
@@ -158,7 +163,16 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
 #pragma unroll
         for (int q = 0; q < QB; ++q) v3_dma(rw, dW + q * 1024, vw[q], (uint32_t)wtap + cso);
         ++is;
-        if (++ics == cps) {
+        if (TI && ntaps > 1) {  // next tap; after the last one, the next channel slice from tap 0
+            if (++it == ntaps) {
+                it = iti = itj = 0;
+                ++ics;
+            } else if (++itj == a.ntw) {
+                itj = 0;
+                ++iti;
+            }
+            if (ics < cps) set_tap();
+        } else if (++ics == cps) {
             ics = 0;
             ++it;
             if (++itj == a.ntw) {
@@ -381,12 +395,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
                                           PFE ? &pf : nullptr);
 }
 
-template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0>
+template <int BM, int BN, int WN, int NS, int NW, int RB, int EB = 2, int FB = 0, bool TI = false>
 int launch_v3(const IGemmArgs& a, hipStream_t st) {
     const int ntiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
     const size_t lds = EB == 4 ? (size_t)NS * (BM + BN) * RB
                                : std::max((size_t)NS * (BM + BN) * RB, epi_lds_bytes(BM, BN, NW * 64));
-    hipLaunchKernelGGL((igemm_v3_kernel<BM, BN, WN, NS, NW, RB, EB, FB>), dim3(ntiles), dim3(NW * 64), lds, st, a);
+    hipLaunchKernelGGL((igemm_v3_kernel<BM, BN, WN, NS, NW, RB, EB, FB, TI>), dim3(ntiles), dim3(NW * 64), lds, st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;

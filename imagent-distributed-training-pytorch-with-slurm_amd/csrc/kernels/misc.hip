@@ -776,6 +776,26 @@ IMK_EXPORT int imk_memset0(void* p, long bytes, void* stream) {
     return 0;
 }
 
+// The stem's bf16 weight shadow [Co][KH][KW][Ci] into its row-segment layout [Co][KH][32] (kw * 4 + ci; the padded
+// channel and taps stay zero), after every optimizer step (one launch instead of an ATen strided copy).
+__global__ __launch_bounds__(256) void stem_pad_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                       int Co, int KH, int KW, int Ci) {
+    const int n = Co * KH * KW * Ci;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+        const int ci = e % Ci, kw = (e / Ci) % KW, r = e / (Ci * KW);  // r = co * KH + kh
+        dst[(size_t)r * 32 + kw * 4 + ci] = src[e];
+    }
+}
+
+IMK_EXPORT int imk_stem_pad(const void* src, void* dst, int Co, int KH, int KW, int Ci, void* stream) {
+    if (Co <= 0 || KH <= 0 || Ci <= 0 || Ci > 4 || KW * 4 > 32) return -100;
+    const int n = Co * KH * KW * Ci;
+    hipLaunchKernelGGL(stem_pad_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src,
+                       (bf16_t*)dst, Co, KH, KW, Ci);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
 IMK_EXPORT int imk_colsum_bf16(const void* x, float* out, int R, int C, void* stream) {
     const int slices = R >= 64 ? min(32, R / 16) : 1;
     hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64, slices), dim3(256), 0, (hipStream_t)stream,

@@ -129,7 +129,12 @@ class NativeState:
             cast_bf16(self.arena.P, self.arena.S)
         self.tplan.run()
         s = self.model.conv1
-        stem_view(s.w_pad, s.kw)[..., : s.in_channels].copy_(s.w_bf16_real)
+        src = s.w_bf16_real
+        if src.is_cuda and src.is_contiguous():
+            _lib.check(_lib.kernels().imk_stem_pad(src.data_ptr(), s.w_pad.data_ptr(), s.out_channels, s.kh, s.kw,
+                                                   s.in_channels, _lib.stream_ptr()), "stem pad")
+        else:
+            stem_view(s.w_pad, s.kw)[..., : s.in_channels].copy_(src)
         if getattr(self, "fp8", None) is not None:
             self.fp8.after_step()
 
@@ -151,16 +156,19 @@ class NativeState:
         S = _lib.STAT_SLOTS
         nbw = _lib.kernels().imk_bn_bwd_scratch_floats(1)
         per = [(2 * S + nbw) * c for c in sizes]        # stats slab + bwd slab/scratch (zeroed)
-        # the Gram-form bn3 backward's accumulators per bottleneck (ops/bn_gram.py): T = g^T h2 [4p][p],
-        # G = h2^T h2 [p][p], colsum(h2) [p] -- zeroed with the slabs by the one per-step memset
+        # the Gram-form bn3 accumulators per bottleneck (ops/bn_gram.py): T = g^T h2 [4p][p], G = h2^T h2 [p][p],
+        # colsum(h2) [p], Q = W3^T diag(B) W3 [p][p], P = W3 Gc [4p][p] -- zeroed with the slabs by the one per-step
+        # memset (the kernels that form them accumulate)
         gram = [(b, b.convs_bns()[-1][0]) for b in self.model.blocks() if len(b.convs_bns()) == 3]
-        gsz = [c3.out_channels * c3.in_channels + c3.in_channels * (c3.in_channels + 1) for _, c3 in gram]
+        gsz = [2 * c3.out_channels * c3.in_channels + c3.in_channels * (2 * c3.in_channels + 1) for _, c3 in gram]
         self.zero_ws = torch.zeros(sum(per) + sum(gsz), dtype=torch.float32, device=self.device)
         go = sum(per)
         for (b, c3), n in zip(gram, gsz):
             C4, p = c3.out_channels, c3.in_channels
             w = self.zero_ws[go:go + n]
-            b._gram_ws = (w[:C4 * p].view(C4, p), w[C4 * p:C4 * p + p * p].view(p, p), w[C4 * p + p * p:])
+            o1, o2, o3, o4 = C4 * p, C4 * p + p * p, C4 * p + p * p + p, C4 * p + 2 * p * p + p
+            b._gram_ws = (w[:o1].view(C4, p), w[o1:o2].view(p, p), w[o2:o3], w[o3:o4].view(p, p),
+                          w[o4:o4 + C4 * p].view(C4, p))
             go += n
         self.save_ws = torch.zeros(sum(4 * c for c in sizes), dtype=torch.float32, device=self.device)
         o = so = 0

@@ -186,6 +186,7 @@ def _declare(name: str, lib) -> None:
             "imk_colsum_bf16": [vp, vp, i32, i32, vp],
             "imk_stem_grad_fold": [vp, vp, i32, i32, i32, i32, vp],
             "imk_memset0": [vp, i64, vp],
+            "imk_stem_pad": [vp, vp, i32, i32, i32, i32, vp],
             "imk_bn_bwd_coef_T": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
             "imk_bn_gram_fwd_stats": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, f32, vp],
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],

@@ -150,7 +150,7 @@ def _dg8(d8, conv):
 
 
 def _gws(block, i):
-    """Entry i (0 T, 1 G, 2 colsum) of the block's zeroed Gram workspace, or None (allocated on demand)."""
+    """Entry i (0 T, 1 G, 2 colsum, 3 Q, 4 P) of the block's zeroed Gram workspace, or None (allocated on demand)."""
     w = getattr(block, "_gram_ws", None)
     return w[i] if w is not None else None
 
@@ -228,7 +228,8 @@ class BlockFn(torch.autograd.Function):
                     ad = _fwd8(ds[0], x, x8, ds[1])
                 ssd = bn_scale_shift(ad, ds[1])
                 res, rsc = ad, ssd[0]
-            aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1], add_shift=ssd[1] if ssd is not None else None)
+            aff, gram_P = gram_fwd_stats(bn, conv, h, h2sum, gws[1], add_shift=ssd[1] if ssd is not None else None,
+                                         P=gws[4])
             out = torch.empty(res.shape, device=res.device, dtype=res.dtype)
             # the ReLU mask of the block output as bits, for the next block's conv1 dgrad epilogue; the output's
             # e4m3 copy from the same epilogue when an fp8 conv reads it
@@ -352,9 +353,9 @@ class BlockFn(torch.autograd.Function):
                 bn_prev = pairs[i - 1][1]
                 fz = BNBwdFuse(acts[i - 1], bn_prev) if fuse else None
                 if isinstance(dA, GramBN):
-                    dH = gram_dgrad(dA, conv, h_in, fz)
+                    dH = gram_dgrad(dA, conv, h_in, fz, Q=_gws(block, 3))
                     g_read = gram_wgrad(conv, dA, h_in, ctx.h2sum, G=_gws(block, 1), P=ctx.gram_P,
-                                         bn=bn_l)  # issued now: it reads dout, which conv1's dgrad
+                                        bn=bn_l, T_out=_gws(block, 0), P_out=_gws(block, 4))  # issued now: it reads dout, which conv1's dgrad
                 else:                                    # accumulates into below
                     dH = igemm_dgrad(dA, conv.wt_bf16, (acts[i - 1].shape[1], acts[i - 1].shape[2]), conv.stride,
                                      conv.padding, conv.kh, conv.kw, bnb=fz, fp8=_dg8(dA8, conv))

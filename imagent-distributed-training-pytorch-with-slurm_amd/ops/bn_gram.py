@@ -83,19 +83,21 @@ def gram_coef(bn, g: torch.Tensor, T: torch.Tensor = None, w3: torch.Tensor = No
     return GramBN(g, coef, T)
 
 
-def gram_P(conv, G: torch.Tensor, s: torch.Tensor, rows: int) -> torch.Tensor:
+def gram_P(conv, G: torch.Tensor, s: torch.Tensor, rows: int, out: torch.Tensor = None) -> torch.Tensor:
     """P = W3 (G - s s^T / rows) [4p][p] fp32: conv3's weight times the CENTRED Gram matrix of h2
-    (``bn_gram_gemm_kernel<0>``), on the current stream."""
+    (``bn_gram_gemm_kernel<0>``, split-K: it accumulates into ``out``, a zeroed [4p][p] -- the per-step workspace --
+    or a fresh zeroed tensor), on the current stream."""
     C4, p = conv.out_channels, conv.in_channels
-    P = torch.empty((C4, p), device=G.device, dtype=torch.float32)
+    P = out if out is not None else torch.zeros((C4, p), device=G.device, dtype=torch.float32)
     _lib.check(_lib.kernels().imk_bn_gram_p(conv.w_bf16.data_ptr(), G.data_ptr(), s.data_ptr(), P.data_ptr(), rows,
                                             C4, p, _lib.stream_ptr()), "bn gram P")
     return P
 
 
-def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tensor:
+def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse, Q: torch.Tensor = None) -> torch.Tensor:
     """dh2 = dx3 W3 without dx3: one v3 GEMM over K = [g (4p) | h2 (p)] with bn2's fused
-    backward epilogue (``bnb``; the bias c W3 enters before its ReLU mask)."""
+    backward epilogue (``bnb``; the bias c W3 enters before its ReLU mask). ``Q``: a zeroed [p][p] fp32 accumulator
+    for W3^T diag(B) W3 (the per-step workspace) or None."""
     N, H, W, C4 = gb.g.shape
     p = h2.shape[-1]
     wt = conv.wt_bf16  # [p][1][1][4p] = W3^T
@@ -106,7 +108,8 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     st = _lib.stream_ptr()
     # Q = W3^T diag(B) W3 [p][p] (symmetric), own fp32 kernel (hipBLASLt ran p = 128 as ONE 128 x 128 workgroup:
     # 36 us alone, 200-360 us in the step beside the weight-gradient stream)
-    Q = torch.empty((p, p), device=h2.device, dtype=torch.float32)
+    if Q is None:
+        Q = torch.zeros((p, p), device=h2.device, dtype=torch.float32)
     _lib.check(k.imk_bn_gram_q(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), p, C4, st), "gram Q")
     _lib.check(k.imk_bn_gram_dgrad_weights(wt.data_ptr(), C4, gb.coef.data_ptr(), Q.data_ptr(), wcat.data_ptr(),
                                            bias.data_ptr(), p, C4, st), "gram dgrad weights")
@@ -123,16 +126,17 @@ def gram_dgrad(gb: GramBN, conv, h2: torch.Tensor, bnb: BNBwdFuse) -> torch.Tens
     return out
 
 
-def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor, add_shift: torch.Tensor = None):
+def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor, add_shift: torch.Tensor = None,
+                   P: torch.Tensor = None):
     """bn3's batch statistics without conv3's output (x3 = h2 W3^T): G = h2^T h2 into the zeroed ``G``, P =
     W3 (G - s s^T / M) (centred), then mean = W3 s / M, var = rowsum(P * W3) / M (``bn_gram_fwd_stats_kernel``)
     into ``bn.work.stats`` / ``save``. Returns (aff [2][4p] = (gamma rstd, beta - mean gamma rstd) for conv3's
     epilogue, P; the weight gradient reuses P). ``add_shift`` [4p]: added to the returned shift (a downsample
-    block's shortcut-BN shift, folded into bn3's)."""
+    block's shortcut-BN shift, folded into bn3's). ``P``: a zeroed [4p][p] accumulator (workspace) or None."""
     C4, p = conv.out_channels, conv.in_channels
     M = h2.numel() // p
     igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
-    P = gram_P(conv, G, s, M)
+    P = gram_P(conv, G, s, M, out=P)
     aff = torch.empty((2, C4), device=h2.device, dtype=torch.float32)
     w = bn.work
     _lib.check(_lib.kernels().imk_bn_gram_fwd_stats(conv.w_bf16.data_ptr(), s.data_ptr(), P.data_ptr(),
@@ -143,12 +147,13 @@ def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor,
 
 
 def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: torch.Tensor = None,
-               P: torch.Tensor = None, bn=None):
+               P: torch.Tensor = None, bn=None, T_out: torch.Tensor = None, P_out: torch.Tensor = None):
     """conv3.weight.grad += A (g^T h2) + B W3 Gc + (c + B mean) colsum(h2) (Gc = the centred Gram matrix of h2;
     ``bn``: bn3, whose saved batch mean enters), on the wgrad side stream.
     ``s``: colsum(h2) if the forward already accumulated it (``bn_act_forward(colsum=)``); ``G``: a zeroed
     [p][p] fp32 accumulator (the per-step workspace) or None; ``P`` = W3 Gc when the forward already formed it
-    (``gram_fwd_stats``): then neither G nor P is recomputed.
+    (``gram_fwd_stats``): then neither G nor P is recomputed. ``T_out`` / ``P_out``: zeroed accumulators for T / P
+    when they are formed here (the per-step workspace), else fresh zeroed tensors.
     Returns the side-stream event after the last read of ``g`` (or None without a side stream):
     the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
     side = streams.side_stream(h2.device) if h2.is_cuda else None
@@ -165,7 +170,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
         ev = None
         T = gb.T
         if T is None:  # (else formed on the main stream for the coefficients: g is not read here)
-            T = torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
+            T = T_out if T_out is not None else torch.zeros((C4, p), device=h2.device, dtype=torch.float32)
             igemm_wgrad(gb.g, h2, T, 1, 0, 1, 1, splits=_splits(C4, p))
             if side is not None:
                 ev = torch.cuda.Event()
@@ -175,7 +180,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
         if own_s:
             colsum_into(h2.view(-1, p), s)
         if P is None:
-            P = gram_P(conv, G, s, h2.numel() // p)
+            P = gram_P(conv, G, s, h2.numel() // p, out=P_out)
         _lib.check(_lib.kernels().imk_bn_gram_wgrad_fixup(conv.weight.grad.data_ptr(), T.data_ptr(), P.data_ptr(),
                                                           gb.coef.data_ptr(), bn.work.save.data_ptr(), s.data_ptr(),
                                                           C4, p, _lib.stream_ptr()), "gram wgrad fixup")

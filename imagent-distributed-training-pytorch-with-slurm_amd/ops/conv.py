@@ -450,7 +450,13 @@ class LinearFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         mod = ctx.mod
         B, Cin = x.shape
-        dyb = dy.to(torch.bfloat16).contiguous().view(B, 1, 1, -1)
+        if dy.dtype == torch.float32 and dy.is_cuda:  # (the xent backward's fp32 gradient: own cast kernel)
+            dyb = torch.empty(dy.shape, device=dy.device, dtype=torch.bfloat16)
+            _lib.check(_lib.kernels().imk_cast_bf16(dy.contiguous().data_ptr(), dyb.data_ptr(), dy.numel(),
+                                                    _lib.stream_ptr()), "cast")
+            dyb = dyb.view(B, 1, 1, -1)
+        else:
+            dyb = dy.to(torch.bfloat16).contiguous().view(B, 1, 1, -1)
         if mod.out_features % 8 == 0:
             dx = igemm_dgrad(dyb, mod.wt_bf16.view(Cin, 1, 1, -1), (1, 1), 1, 0, 1, 1).view(B, Cin)
         else:  # the gather GEMM needs 16-B channel chunks; a class count like 100 takes a library GEMM

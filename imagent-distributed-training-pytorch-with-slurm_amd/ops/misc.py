@@ -136,11 +136,13 @@ class XentFn(torch.autograd.Function):
     def backward(ctx, gout):
         logits, labels, lse = ctx.saved_tensors
         B, NC = logits.shape
-        dz = torch.empty((B, NC), device=logits.device, dtype=torch.bfloat16)
         g = gout.to(torch.float32).contiguous()
-        _lib.check(_lib.kernels().imk_xent_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(),
-                                               g.data_ptr(), dz.data_ptr(), B, NC,
-                                               float(ctx.smoothing), _lib.stream_ptr()), "xent bwd")
+        # the logits' own dtype (fp32): autograd would otherwise cast a bf16 gradient back with an ATen copy; the
+        # linear layer's backward rounds it to bf16 with its own kernel
+        dz = torch.empty((B, NC), device=logits.device, dtype=logits.dtype)
+        fn = _lib.kernels().imk_xent_bwd_f32 if logits.dtype == torch.float32 else _lib.kernels().imk_xent_bwd
+        _lib.check(fn(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), g.data_ptr(), dz.data_ptr(), B, NC,
+                      float(ctx.smoothing), _lib.stream_ptr()), "xent bwd")
         return dz, None, None, None
 
 
