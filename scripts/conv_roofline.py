@@ -69,7 +69,7 @@ def main():
     recs = [json.loads(l) for l in open(a.log)]
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, dispatch_id, start, end, stream_id from kernels order by dispatch_id").fetchall()
-    conv = [r for r in rows if any(k in r[0] for k in CONV_KERNELS)]
+    conv = [r for r in rows if any(k in r[0] for k in CONV_KERNELS) and "fixup" not in r[0]]
     need = sum(r["kernels"] for r in recs)
     if need != len(conv):
         raise SystemExit(f"log has {need} conv dispatches, trace {len(conv)}: not the same run?")
