@@ -85,8 +85,8 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         return -104;
     if (a.flags & IG_STEM) {  // C == 4 row-segment gather, K = KH x 32
         if (a.C != 4 || a.ntw > 8 || a.dhs != 1 || a.dws != 1) return -102;
-        if (tile == 0) {  // streaming stem (conv_stream.hip)
-            const int r = conv_stream(a, st);
+        if (tile == 0 || tile == 23) {  // band stem (tile 0) / streaming row-segment stem (23), conv_stream.hip
+            const int r = conv_stem(a, st, tile);
             if (r != 1) return r;
         }
         return launch_rs<128, 64, 1, 2>(a, st);

@@ -1217,6 +1217,7 @@ int conv_igemm_fp8(const IGemmArgs& a, int tile, hipStream_t st);
 // short-K (C in {64, 128}) 1x1 convolutions as an HBM stream (conv_stream.hip);
 // returns 1 when the shape / flags are not covered
 int conv_stream(const IGemmArgs& a, hipStream_t st, int bn = 0);
+int conv_stem(const IGemmArgs& a, hipStream_t st, int tile);
 // 64 -> 64 3x3 stride-1 convs (fwd and dgrad) with weights and an input halo patch resident in
 // LDS (conv_halo.hip); returns 1 when the shape / flags are not covered
 int conv_halo(const IGemmArgs& a, hipStream_t st);

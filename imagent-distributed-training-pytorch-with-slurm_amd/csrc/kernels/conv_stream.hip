@@ -471,7 +471,200 @@ int launch_stream(const IGemmArgs& a, hipStream_t st) {
     return 1;
 }
 
+// The 7x7 / stride-2 stem (C = 4 padded channels -> 64) as a band kernel: a persistent block stages R output rows'
+// worth of input rows (2R + 5 rows x the full padded width, 4 channels) in LDS ONCE and builds every B fragment
+// from there -- a kernel row's 8 taps x 4 channels of one output pixel are 64 contiguous LDS bytes -- instead of
+// gathering two 8-B pieces per tap row per pixel from L1/L2 (each input pixel fed ~12 output pixels: the
+// streaming stem ran at 2.0 TB/s, 1.06 ms per call at 1024 img, profiles/r50_b1024_r5_standalone.md). Weights
+// (64 x 7 x 32) live in registers (28 A fragments per lane). The next band's rows are loaded into registers
+// while the current band computes, then written to the other LDS buffer. Epilogue as the streaming kernel's
+// (wave-private swizzled LDS transpose -> coalesced 16-B stores, shifted forward statistics, or the eval
+// forward's folded BatchNorm + ReLU).
+// Layout: LDS input row pitch SP = 232 pixels x 8 B; input column c at byte (c + 4) * 8 (columns -4 .. -1 and
+// W .. W + 3 stay zero: the padding taps and the zero-weight 8th tap read finite zeros).
+template <int R>
+__global__ __launch_bounds__(256, 2) void stem_band_kernel(const IGemmArgs a, int nbands) {
+    constexpr int KH = 7, KS = 7, FN = 4;             // kernel rows (= MFMA k-steps), 64 / 16 channel fragments
+    constexpr int PR = 2 * R + KH - 2;                  // staged input rows per band
+    constexpr int SP = 232 * 8;                         // LDS row pitch, bytes
+    constexpr int BUF = PR * SP;
+    constexpr int EP = 64 * 2;                          // epilogue row pitch (64 channels)
+    constexpr int W16 = 112;                            // 16-B chunks per input row (224 px x 8 B)
+    constexpr int NCH = PR * W16;                       // chunks per band
+    constexpr int CPT = (NCH + 255) / 256;              // chunks per thread
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* sE = smem + 2 * BUF + (threadIdx.x >> 6) * 16 * EP;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int bpi = (a.OH + R - 1) / R;  // bands per image
+
+    // zero both buffers once (padding columns stay zero: the band loads write columns 0 .. W-1 only)
+    for (int e = tid; e < 2 * BUF / 16; e += 256) reinterpret_cast<u32x4*>(smem)[e] = u32x4{0u, 0u, 0u, 0u};
+    // weights: A fragment (kernel row ks, channel fragment i) = Wk[i * 16 + fr][ks * 32 + fq * 8 .. + 8]
+    bf16x8 wa[KS][FN];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+            wa[ks][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
+                                                       a.Wk + (size_t)(i * 16 + fr) * a.ldb + ks * 32 + fq * 8));
+    // epilogue constants of this lane's fixed channel chunk
+    const int cc = lane & 7, n = cc * 8;
+    const bool affine = a.flags & IG_AFFINE, relu = a.flags & IG_RELU;
+    float mean[8], sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        mean[c] = (a.stats && a.shift) ? a.shift[n + c] : 0.f;
+        sc[c] = affine ? a.bias[n + c] : 1.f;
+        sh[c] = affine ? a.bias[a.Nout + n + c] : 0.f;
+        s1[c] = s2[c] = 0.f;
+    }
+
+    u32x4 stage[CPT];
+    auto load_band = [&](int band) {  // global -> registers
+        const int img = band / bpi, oy0 = (band - img * bpi) * R;
+        const int iy0 = 2 * oy0 - 3;
+#pragma unroll
+        for (int t = 0; t < CPT; ++t) {
+            const int e = tid + 256 * t;
+            const int r = e / W16, c16 = e - r * W16, iy = iy0 + r;
+            const bool ok = e < NCH && (unsigned)iy < (unsigned)a.H;
+            stage[t] = ok ? *reinterpret_cast<const u32x4*>(a.X + (((size_t)img * a.H + iy) * a.W) * 4 + c16 * 8)
+                          : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    auto store_band = [&](int buf) {  // registers -> LDS (column 0 at byte 32)
+#pragma unroll
+        for (int t = 0; t < CPT; ++t) {
+            const int e = tid + 256 * t;
+            if (e < NCH) {
+                const int r = e / W16, c16 = e - r * W16;
+                *reinterpret_cast<u32x4*>(smem + buf * BUF + r * SP + 32 + c16 * 16) = stage[t];
+            }
+        }
+    };
+
+    int band = blockIdx.x;
+    if (band < nbands) load_band(band);
+    __syncthreads();  // (the zero fill)
+    if (band < nbands) store_band(0);
+    __syncthreads();
+    int buf = 0;
+    for (; band < nbands; band += gridDim.x) {
+        const int nxt = band + gridDim.x;
+        if (nxt < nbands) load_band(nxt);  // in flight under this band's MFMAs
+        const int img = band / bpi, oy0 = (band - img * bpi) * R;
+        const char* sb = smem + buf * BUF;
+        const int rows = min(R, a.OH - oy0);
+        const int ngroups = rows * (a.OW / 16);
+        for (int g = wid; g < ngroups; g += 4) {
+            const int ry = g / (a.OW / 16), ox0 = (g - ry * (a.OW / 16)) * 16;
+            const int ox = ox0 + fr;
+            f32x4 acc[FN];
+#pragma unroll
+            for (int i = 0; i < FN; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                // taps 2fq, 2fq + 1 of kernel row ks: input row 2 (oy0 + ry) + ks - 3 = staged row 2 ry + ks,
+                // columns 2 ox - 3 + 2 fq .. + 1 at byte (2 ox + 1 + 2 fq) * 8
+                const char* pb = sb + (2 * ry + ks) * SP + (2 * ox + 1 + 2 * fq) * 8;
+                const u32x2 lo = *reinterpret_cast<const u32x2*>(pb);
+                const u32x2 hi = *reinterpret_cast<const u32x2*>(pb + 8);
+                const bf16x8 fb = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+#pragma unroll
+                for (int i = 0; i < FN; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][i], fb, acc[i], 0, 0, 0);
+            }
+            // (1) fragments -> wave-private LDS rows (pixel fr, channels i * 16 + 4 fq .. + 3), swizzled
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+                *reinterpret_cast<u32x2*>(sE + fr * EP + epi_swz(fr, (i * 16 + fq * 4) * 2)) =
+                    u32x2{pack_bf2(acc[i][0], acc[i][1]), pack_bf2(acc[i][2], acc[i][3])};
+            __builtin_amdgcn_wave_barrier();
+            // (2) row chunks: pixel q * 8 + lane / 8, channels n .. n + 7
+            const long m0 = ((long)img * a.OH + oy0 + ry) * a.OW + ox0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int p = q * 8 + (lane >> 3);
+                const u32x4 t = epi_read(sE, p, EP, cc);
+                float v[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[2 * k] = fmaf(lo_bf(t[k]), sc[2 * k], sh[2 * k]);
+                    v[2 * k + 1] = fmaf(hi_bf(t[k]), sc[2 * k + 1], sh[2 * k + 1]);
+                    if (relu) {
+                        v[2 * k] = fmaxf(v[2 * k], 0.f);
+                        v[2 * k + 1] = fmaxf(v[2 * k + 1], 0.f);
+                    }
+                }
+                u32x4 o;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+                *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + (m0 + p) * a.ldy + n) = o;
+                if (a.stats) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {  // statistics of the stored (bf16) values
+                        const float d = (c & 1 ? hi_bf(o[c >> 1]) : lo_bf(o[c >> 1])) - mean[c];
+                        s1[c] += d;
+                        s2[c] += d * d;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // buffer buf ^ 1 was last read in the previous band, which every wave finished before the barrier below in
+        // that iteration; the barrier orders these stores before the next band's reads
+        if (nxt < nbands) store_band(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    if (!a.stats) return;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+            s1[c] += __shfl_xor(s1[c], o, 64);
+            s2[c] += __shfl_xor(s2[c], o, 64);
+        }
+    }
+    if (lane >= 8) return;
+    float* st = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * a.Nout;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        atomicAdd(st + n + c, s1[c]);
+        atomicAdd(st + a.Nout + n + c, s2[c]);
+    }
+}
+
+// the band stem's shapes: 4-channel 224-wide input, 7x7 / stride 2 / pad 3, 64 channels, 16 | OW, dense bf16 output
+bool stem_band_ok(const IGemmArgs& a) {
+    if (a.flags & (IG_OUT_F32 | IG_FP8 | IG_ACCUM | IG_BNBWD | IG_NOSTREAM | IG_RES | IG_MASKOUT | IG_Q8OUT)) return false;
+    if ((a.flags & IG_RELU) && !(a.flags & IG_AFFINE)) return false;
+    if ((a.bias && !(a.flags & IG_AFFINE)) || a.xbn || a.X2) return false;
+    return a.C == 4 && a.W == 224 && a.nth == 7 && a.ntw == 7 && a.sA == 2 && a.dh0 == -3 && a.dw0 == -3 &&
+           a.dhs == 1 && a.dws == 1 && a.Nout == 64 && a.ldb == 7 * 32 && a.ldy == 64 && a.OW % 16 == 0 &&
+           2 * (a.OW - 1) - 3 + 8 <= a.W + 3 && a.sY == 1 && a.YH == a.OH && a.YW == a.OW && a.oy == 0 && a.ox == 0;
+}
+
+int launch_stem_band(const IGemmArgs& a, hipStream_t st) {
+    constexpr int R = 4;
+    const size_t lds = 2 * (size_t)(2 * R + 5) * 232 * 8 + 4 * 16 * 64 * 2;
+    static int resident = 0;
+    if (resident == 0) resident = resident_blocks(stem_band_kernel<R>, lds);
+    const int nbands = a.N * ((a.OH + R - 1) / R);
+    hipLaunchKernelGGL((stem_band_kernel<R>), dim3(std::min(nbands, resident)), dim3(256), lds, st, a, nbands);
+    CONV_COUNTED();
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
 }  // namespace
+
+// the 7x7 stem forward: the band kernel (tile 0) or the streaming row-segment kernel (tile 23, A/B); 1: not covered
+int conv_stem(const IGemmArgs& a, hipStream_t st, int tile) {
+    if (tile == 0 && stem_band_ok(a)) return launch_stem_band(a, st);
+    return conv_stream(a, st, 0);
+}
 
 // Returns 1 if the shape is not one this kernel covers (caller falls back).
 // bn: channel-slice width (0 auto: the widest that divides Nout; 64/128/256 forced)

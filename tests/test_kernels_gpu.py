@@ -329,6 +329,43 @@ def test_stem_stats_persistent_blocks():
     assert rel(slab.sum(0)[1], (yb * yb).sum(0)) < 1e-4
 
 
+@pytest.mark.parametrize("N", [1, 5])
+def test_stem_band_matches_stream(N):
+    """The band stem (conv_stream.hip stem_band_kernel: input rows staged in LDS once per 4 output rows, weights in
+    registers) against the streaming row-segment stem (tile 23) and fp32: training forward with shifted
+    statistics, and the eval forward's folded BatchNorm + ReLU; image borders on every side."""
+    from imagent_amd.ops.conv import igemm_fwd
+    torch.manual_seed(9)
+    H, Co = 224, 64
+    x4 = torch.zeros(N, H, H, 4, device=DEV, dtype=torch.bfloat16)
+    x4[..., :3] = bf(torch.randn(N, H, H, 3, device=DEV) + 0.3)
+    w3 = bf(torch.randn(Co, 3, 7, 7, device=DEV) * 0.1)
+    wrow = torch.zeros(Co, 7, 32, device=DEV, dtype=torch.bfloat16)
+    wrow[:, :, :28].view(Co, 7, 7, 4)[..., :3] = w3.permute(0, 2, 3, 1)
+    ref = F.conv2d(nchw(x4[..., :3]).float(), w3.float(), None, 2, 3)
+    from imagent_amd.models.resnet import BNWork
+    from imagent_amd.ops import _lib
+    shift = torch.randn(Co, device=DEV) * 0.1
+    outs = {}
+    for tile in (0, 23):
+        work = BNWork(torch.zeros(32, 2, Co, device=DEV), torch.zeros(2, Co, device=DEV),
+                      torch.stack([shift, torch.ones(Co, device=DEV)]),
+                      torch.zeros(_lib.kernels().imk_bn_bwd_scratch_floats(Co), device=DEV))
+        y = igemm_fwd(x4, wrow, 2, 3, 7, 7, stats=work, stem=True, tile=tile)
+        outs[tile] = (y, work.slab.sum(0))
+    y0, st0 = outs[0]
+    y1, st1 = outs[23]
+    assert rel(nchw(y0), ref) < 1e-2
+    assert rel(y0.float(), y1.float()) < 1e-3
+    d = y0.float().reshape(-1, Co) - shift
+    assert rel(st0[0], d.sum(0)) < 1e-4 and rel(st0[1], (d * d).sum(0)) < 1e-4
+    # eval: folded BN (scale, shift) + ReLU in the epilogue
+    aff = torch.stack([torch.rand(Co, device=DEV) + 0.5, torch.randn(Co, device=DEV) * 0.2]).contiguous()
+    ye = igemm_fwd(x4, wrow, 2, 3, 7, 7, stem=True, affine=aff, relu=True)
+    want = torch.relu(y0.float() * aff[0] + aff[1])
+    assert rel(ye.float(), want) < 1e-2
+
+
 def test_maxpool_stem_size():
     """The stem's pool at a full-size row (112 px, 64 ch): row-grid indexing."""
     from imagent_amd.ops.misc import MaxPoolFn
