@@ -39,7 +39,7 @@ def _shapes(arch, size, batch):
 
 SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _shapes("resnet18", 448, 128)
 
-# conv kernel templates in the R50 bench trace (round 4 HEAD, profiles/r50_b1024_v21_stream_tables.md: v3 with its
+# conv kernel templates in the R50 bench trace (round 5 HEAD, profiles/r50_b1024_r5_standalone.md: v3 with its
 # element-size / format template arguments, the streaming kernel with its second-K-segment width); update together
 # with the dispatcher. Not listed (no plain conv shape takes them; tests/test_model_gpu.py covers them against the
 # fp32 model in test_bn_gram_backward_matches_torch and test_fp8_forward_training_step[resnet50-gram]): the
@@ -48,7 +48,6 @@ SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _sh
 BENCH_KERNELS = [
     "conv_stream_kernel<128, 128, 2, 1, false, false, 0>",
     "conv_stream_kernel<128, 128, 2, 3, false, false, 0>",
-    "conv_stream_kernel<224, 64, 2, 0, true, false, 0>",
     "conv_stream_kernel<256, 64, 2, 0, false, false, 0>",
     "conv_stream_kernel<256, 64, 2, 1, false, false, 0>",
     "conv_stream_kernel<256, 64, 2, 3, false, false, 0>",
@@ -60,11 +59,12 @@ BENCH_KERNELS = [
     "halo3x3_kernel<56, 4, 1>",
     "igemm_dma_kernel<128, 128, 2, 2, 0, 4, 0, 2, 0, 128>",
     "igemm_dma_kernel<128, 128, 2, 2, 1, 4, 2, 2, 0, 128>",
-    "igemm_v3_kernel<128, 128, 2, 2, 4, 128, 2, 0>",
-    "igemm_v3_kernel<256, 256, 2, 2, 8, 128, 2, 0>",
-    "wgrad_halo_kernel<14, 14, 7, 16, 1>",
-    "wgrad_halo_kernel<28, 4, 4, 32, 1>",
-    "wgrad_halo_kernel<56, 4, 7, 64, 1>",
+    "igemm_v3_kernel<128, 128, 2, 2, 4, 128, 2, 0, false>",
+    "igemm_v3_kernel<256, 256, 2, 2, 8, 128, 2, 0, false>",
+    "stem_band_kernel<4>",
+    "wgrad_halo_kernel<14, 14, 7, 16>",
+    "wgrad_halo_kernel<28, 4, 4, 32>",
+    "wgrad_halo_kernel<56, 4, 7, 64>",
     "wgrad_kernel<128, 128, 2, false, 4, 32, false>",
     "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
@@ -84,7 +84,7 @@ def _kernels(fn):
         out = fn()
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
-    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_", "halo3x3"))]
+    return out, [n for n in names if any(k in n for k in ("igemm", "conv_stream", "wgrad_", "halo3x3", "stem_band"))]
 
 
 def _short(names):
