@@ -18,6 +18,15 @@
 //    one pixel) is ONE 16-B global load -- no LDS staging at all. D groups
 //    are prefetched into registers ahead of use (bytes in flight per CU ~
 //    8 waves x D x 2-4 KB);
+//  * every global access of the group loop is a raw BUFFER load / store off a wave-uniform base (the group's
+//    first row) with per-lane 32-bit offsets; rows past M and groups past the end are out-of-range offsets
+//    (loads read zeros, stores are dropped), so the loop has no divergent memory branch. With the former
+//    predicated pointer loads the compiler's waitcnt bookkeeping fell back to s_waitcnt vmcnt(0) around them
+//    (277 of them in the fused-output kernel), draining the prefetch in every group's epilogue; now the
+//    epilogue's own operands (BN-backward x / mask, residual) are issued before the next prefetch and waited
+//    for with a counted vmcnt (round 5: <64,256> fused output 870 -> 742 us, <128,128> 508 -> 380 us in-step);
+//  * the weight fragments go through a register ring read several MFMAs ahead (sched_group_barrier pins the
+//    interleave; left alone the scheduler issued each ds_read right before its MFMA and waited for it);
 //  * v_mfma_f32_16x16x32_bf16, weights = A (rows = output channels);
 //  * epilogue per group: the 16 x BN bf16 tile goes through a wave-private LDS
 //    buffer and comes back as 16-B row chunks, so every global store / read of
@@ -33,6 +42,16 @@
 #include "conv_igemm_impl.h"
 
 namespace {
+
+// raw buffer access of the streaming loop: num_records 2^31 - 1, or 0 for an operand the launch does not use
+// (its loads read zeros, its stores are dropped); per-lane offsets >= SOOB are out of range (rows past M)
+constexpr uint32_t SOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s_rsrc(const void* p, bool on) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, on ? 0x7FFFFFFF : 0, 0x00020000);
+}
+__device__ __forceinline__ u32x4 s_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
 
 // MODE 0: plain epilogue (+ optional IG_ACCUM); IG_BNBWD with the ReLU mask
 // from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3); 4: the plain epilogue with
@@ -72,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     constexpr int QB = bnb ? NR : (NR < 4 ? NR : 4);
     static_assert(!bnb || NR <= 4, "BN-backward epilogue: slices of <= 128 channels");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     char* sW = smem;
     char* sE = smem + BN * RB + wid * 16 * EP;
 
@@ -187,25 +206,35 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
             return;
         }
-        size_t row = 0;
+        // branch-free: buffer loads off a wave-uniform base (the group's first input row); rows past M and groups
+        // past the end read zeros through an out-of-range offset (no divergent load, so the compiler's vmcnt
+        // bookkeeping stays exact and the prefetch stays in flight, see the header)
+        const bool gok = g < ngroups;
+        const int m0 = gok ? g * 16 : 0;
+        size_t row0 = m0;
+        if (!dense) {
+            const int img = m0 / ohw, rem = m0 - img * ohw;
+            const int oh = rem / a.OW, ow = rem - oh * a.OW;
+            row0 = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
+        }
+        uint32_t off = SOOB;
         if (ok) {
-            if (dense) {
-                row = (size_t)m;
-            } else {
+            size_t row = (size_t)m;
+            if (!dense) {
                 const int img = m / ohw, rem = m - img * ohw;
                 const int oh = rem / a.OW, ow = rem - oh * a.OW;
                 row = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
             }
+            off = (uint32_t)((row - row0) * a.C * 2) + fq * 16;
         }
-        const bf16_t* p = a.X + row * a.C + fq * 8;
+        const __amdgpu_buffer_rsrc_t rx = s_rsrc(a.X + row0 * a.C, true);
 #pragma unroll
-        for (int ks = 0; ks < KS1; ++ks)
-            pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(p + ks * 32) : u32x4{0u, 0u, 0u, 0u};
+        for (int ks = 0; ks < KS1; ++ks) pf[d][ks] = s_ld16(rx, off + ks * 64);
         if constexpr (K2 > 0) {  // (dense rows only: host check)
-            const bf16_t* p2 = a.X2 + row * K2 + fq * 8;
+            const __amdgpu_buffer_rsrc_t rx2 = s_rsrc(a.X2 + (size_t)m0 * K2, true);
+            const uint32_t off2 = ok ? (uint32_t)(fr * K2 * 2 + fq * 16) : SOOB;
 #pragma unroll
-            for (int ks = KS1; ks < KS; ++ks)
-                pf[d][ks] = ok ? *reinterpret_cast<const u32x4*>(p2 + (ks - KS1) * 32) : u32x4{0u, 0u, 0u, 0u};
+            for (int ks = KS1; ks < KS; ++ks) pf[d][ks] = s_ld16(rx2, off2 + (ks - KS1) * 64);
         }
     };
 #pragma unroll
@@ -234,8 +263,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     for (int g0 = w0; g0 < ngroups; g0 += D * wstride) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const int g = g0 + d * wstride;
-            if (g >= ngroups) break;
+            const int g = g0 + d * wstride;  // past the end: every access out of range (no divergent exit)
             bf16x8 fb[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
@@ -250,51 +278,72 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     fb[ks] = __builtin_bit_cast(bf16x8, pf[d][ks]);
                 }
             }
-            fetch(d, g + D * wstride);
-            long e[NR];
+            // the group's epilogue operands: wave-uniform bases at the group's pixel row, per-lane byte offsets
+            // (rows past M: out of range, loads read zeros and stores are dropped). Every load of the loop body is
+            // unconditional, so the prefetch below stays in flight through the epilogue's waits
+            const size_t eb0 = (size_t)(g < ngroups ? g * 16 : 0) * a.ldy;
+            const bf16_t* ybase = reinterpret_cast<const bf16_t*>(a.Y) + eb0;
+            const __amdgpu_buffer_rsrc_t ry = s_rsrc(ybase, true);
+            const __amdgpu_buffer_rsrc_t ro = s_rsrc(accum ? ybase : a.bnx + eb0, accum || resid);
+            const __amdgpu_buffer_rsrc_t rbx = s_rsrc(a.bnx + eb0, bnb && a.bnx);
+            const __amdgpu_buffer_rsrc_t rx2o = s_rsrc(a.bnx2 + eb0, has_x2);
+            const __amdgpu_buffer_rsrc_t rym = s_rsrc(a.bnym + eb0 / 8, has_y || maskout);
+            const __amdgpu_buffer_rsrc_t ry8 = s_rsrc(reinterpret_cast<const uint8_t*>(a.Y8) + eb0, q8out);
+            constexpr bool early = bnb || FO;
+            bool ev[NR];
+            uint32_t o2[NR];
             u32x4 oo[NR], xo[NR], x2o[NR];
             uint32_t yo[NR];
             auto issue = [&](int u) {
-                const int m = g * 16 + u * PPR + lane / CH;
-                e[u] = m < a.M ? (long)m * a.ldy + n : -1;
-                if (e[u] >= 0) {
-                    if (resid) oo[u] = *reinterpret_cast<const u32x4*>(a.bnx + e[u]);
-                    if (accum) {
-                        bool ok = true;
-                        if (a.flags & IG_ACCUM_SUB2) {  // dense output grid: (oh, ow) of row m
-                            const int rem = m % ohw, oh = rem / a.OW;
-                            ok = ((oh | (rem - oh * a.OW)) & 1) == 0;
-                        }
-                        oo[u] = ok ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(a.Y) + e[u])
-                                   : u32x4{0u, 0u, 0u, 0u};
-                    }
-                    if (bnb) {
-                        // bnx null (mask bits given): slot 0 of the slab is then not sum(g xhat) (bn_gram.hip forms
-                        // it from g^T h2) and x is never read
-                        xo[u] = a.bnx ? *reinterpret_cast<const u32x4*>(a.bnx + e[u]) : u32x4{0u, 0u, 0u, 0u};
-                        if (has_y) yo[u] = a.bnym[e[u] >> 3];
-                        if (has_x2) x2o[u] = *reinterpret_cast<const u32x4*>(a.bnx2 + e[u]);
-                    }
+                const int pr = u * PPR + lane / CH;
+                const int m = g * 16 + pr;
+                ev[u] = g < ngroups && m < a.M;
+                const uint32_t rel = (uint32_t)(pr * a.ldy + n);  // elements from eb0
+                o2[u] = ev[u] ? rel * 2 : SOOB;
+                uint32_t oo_off = o2[u];
+                if (accum && (a.flags & IG_ACCUM_SUB2)) {  // dense output grid: only even (oh, ow) accumulate
+                    const int rem = m % ohw, oh = rem / a.OW;
+                    if (((oh | (rem - oh * a.OW)) & 1) != 0) oo_off = SOOB;
+                }
+                if (early || accum) oo[u] = s_ld16(ro, oo_off);  // (plain mode: a uniform branch, late in the epilogue)
+                if (bnb) {
+                    // bnx null (mask bits given): slot 0 of the slab is then not sum(g xhat) (bn_gram.hip forms
+                    // it from g^T h2) and x is never read (zeros)
+                    xo[u] = s_ld16(rbx, o2[u]);
+                    if (has_y) yo[u] = __builtin_amdgcn_raw_buffer_load_b8(rym, ev[u] ? rel >> 3 : SOOB, 0, 0);
+                    if (has_x2) x2o[u] = s_ld16(rx2o, o2[u]);
                 }
             };
-            // the BN-backward (x / mask) and residual reads go out before the MFMAs: their latency hides behind
-            // the group's MFMAs (the accumulated old output too measured slower: eval 52.8k -> 48.9k val img/s,
-            // deterministic 11.7k -> 11.2k img/s)
-            const bool early = bnb || resid;
-            if (early) {
+            // the BN-backward (x / mask) and residual reads go out before the MFMAs and BEFORE the next prefetch:
+            // waiting for them leaves the prefetch in flight (the accumulated old output of the plain mode is read
+            // in the epilogue: issued early it measured slower, eval 52.8k -> 48.9k val img/s)
+            if constexpr (early) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u) issue(u);
             }
+            fetch(d, g + D * wstride);
             f32x4 acc[FN];
 #pragma unroll
             for (int i = 0; i < FN; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // weight fragments through a ring of RR registers, read RR - 1 MFMAs ahead of use, MFMA t = (k-step
+            // t / FN, channel fragment t % FN) (the group barriers pin the interleave: left to itself the scheduler
+            // issued each ds_read right before its MFMA and waited for it, a full LDS latency per MFMA)
+            constexpr int NT = KS * FN, RR = NT < 8 ? NT : FN >= 16 && (FO || XBN) ? 3 : (FN >= 16 || MODE == 3 ? 4 : 8);
+            bf16x8 fa[RR];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
+            for (int t = 0; t < RR - 1; ++t)
+                fa[t] = *reinterpret_cast<const bf16x8*>(sW + (t % FN) * 16 * RB + aoff[t / FN]);
+            __builtin_amdgcn_sched_group_barrier(0x100, RR - 1, 0);
 #pragma unroll
-                for (int i = 0; i < FN; ++i) {
-                    const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sW + i * 16 * RB + aoff[ks]);
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[ks], acc[i], 0, 0, 0);
+            for (int t = 0; t < NT; ++t) {
+                if (t + RR - 1 < NT) {
+                    const int u = t + RR - 1;
+                    fa[u % RR] = *reinterpret_cast<const bf16x8*>(sW + (u % FN) * 16 * RB + aoff[u / FN]);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
+                acc[t % FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t % RR], fb[t / FN], acc[t % FN], 0, 0, 0);
+                __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            }
             // (1) fragments -> wave-private LDS rows (pixel fr, 4 channels per lane).
             // DS instructions of one wave execute in order: the re-reads below see
             // these writes, and the previous group's reads are complete (their
@@ -307,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             // (2) coalesced row chunks: pixel q*PPR + lane/CH, channels n .. n+7
 #pragma unroll
             for (int q0 = 0; q0 < NR; q0 += QB) {
-                if (!early) {
+                if constexpr (!early) {
 #pragma unroll
                     for (int u = 0; u < QB; ++u) issue(q0 + u);
                 }
@@ -316,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     const int q = q0 + u;
                     const int p = q * PPR + lane / CH;
                     const u32x4 t = epi_read(sE, p, EP, cc);
-                    if (e[q] < 0) continue;
+                    const float vf = ev[q] ? 1.f : 0.f;  // rows past M: stores dropped, statistics masked
                     float v[8];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -358,7 +407,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     u32x4 o;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
-                    *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.Y) + e[q]) = o;
+                    __builtin_amdgcn_raw_buffer_store_b128(o, ry, o2[q], 0, 0);
                     if (q8out) {  // quantise the bf16-rounded values the bf16 consumers see
                         float w[8];
 #pragma unroll
@@ -367,10 +416,11 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             w[2 * k + 1] = hi_bf(o[k]);
                         }
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) m8 = fmaxf(m8, fabsf(w[i]));
-                        *reinterpret_cast<u32x2*>(reinterpret_cast<uint8_t*>(a.Y8) + e[q]) =
+                        for (int i = 0; i < 8; ++i) m8 = fmaxf(m8, fabsf(w[i]) * vf);
+                        __builtin_amdgcn_raw_buffer_store_b64(
                             u32x2{pack4_fp8(w[0] * q8s, w[1] * q8s, w[2] * q8s, w[3] * q8s),
-                                  pack4_fp8(w[4] * q8s, w[5] * q8s, w[6] * q8s, w[7] * q8s)};
+                                  pack4_fp8(w[4] * q8s, w[5] * q8s, w[6] * q8s, w[7] * q8s)},
+                            ry8, ev[q] ? o2[q] / 2 : SOOB, 0, 0);
                     }
                     if (maskout) {  // stored bf16 > 0: nonzero, sign clear, not NaN (as bn_fwd's ym)
                         uint32_t b = 0;
@@ -379,13 +429,13 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             const uint32_t h = (o[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
                             b |= (h != 0u && h <= 0x7F80u ? 1u : 0u) << i;
                         }
-                        const_cast<uint8_t*>(a.bnym)[e[q] >> 3] = (uint8_t)b;
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rym, ev[q] ? o2[q] / 16 : SOOB, 0, 0);
                     }
                     if (a.stats) {
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {  // statistics of the stored (bf16) values
-                            v[2 * k] = lo_bf(o[k]);
-                            v[2 * k + 1] = hi_bf(o[k]);
+                            v[2 * k] = lo_bf(o[k]) * vf;
+                            v[2 * k + 1] = hi_bf(o[k]) * vf;
                         }
                         if (bnb) {
 #pragma unroll
@@ -403,7 +453,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                         } else {
 #pragma unroll
                             for (int c = 0; c < 8; ++c) {
-                                const float d = v[c] - mean[c];
+                                const float d = (v[c] - mean[c]) * vf;
                                 s1[c] += d;
                                 s2[c] += d * d;
                             }
@@ -705,7 +755,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
             a.H != a.OH || a.W != a.OW || a.sY != 1 || a.YH != a.OH || a.YW != a.OW || a.ldy != a.Nout ||
             a.ldb < a.C || a.dh0 != 0 || a.dw0 != 0)
             return -120;
-        if (a.C == 64 && a.Nout % 256 == 0) return launch_stream1<64, 256, 3, 0, false, true>(a, st);
+        if (a.C == 64 && a.Nout % 256 == 0) return launch_stream1<64, 256, 2, 0, false, true>(a, st);
         if (a.C == 64 && a.Nout % 128 == 0) return launch_stream1<64, 128, 3, 0, false, true>(a, st);
         if (a.C == 128 && a.Nout % 128 == 0) return launch_stream1<128, 128, 2, 0, false, true>(a, st);
         return -120;
@@ -734,7 +784,10 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     if (bn == 0) bn = maxbn;
     while (bn > 64 && (bn > maxbn || a.Nout % bn)) bn >>= 1;
     if (a.C == 64) {
-        if (bn == 256) return launch_stream<64, 256, 3>(a, st);
+        // 256-channel slices: the fused-output / operand-BN variants prefetch 2 groups (3 spill at 256 VGPRs)
+        if (bn == 256)
+            return (a.flags & (IG_RES | IG_MASKOUT | IG_Q8OUT)) ? launch_stream1<64, 256, 2, 4>(a, st)
+                                                                : launch_stream1<64, 256, 3, 0>(a, st);
         if (bn == 128) return launch_stream<64, 128, 3>(a, st);
         return launch_stream<64, 64, 3>(a, st);
     }
