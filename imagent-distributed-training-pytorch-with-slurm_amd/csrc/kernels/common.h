@@ -50,6 +50,21 @@ __device__ __forceinline__ float wave_max(float v) {
 // must be bijective"): blocks that the dispatcher deals to the same XCD
 // (b % 8 equal) get a contiguous range of logical tile ids, so neighbouring
 // tiles that share operand panels hit the same 4 MiB L2.
+// raw buffer access: num_records 2^31 - 1 (or 0 for an operand a launch does not use: loads read zeros, stores
+// are dropped); per-lane offsets >= BUF_OOB are out of range. Branch-free predication for the streaming loops:
+// a predicated pointer load puts the load under a divergent branch, and the compiler's waitcnt bookkeeping then
+// falls back to s_waitcnt vmcnt(0) around it, draining every prefetch in flight (conv_stream.hip, conv_halo.hip)
+constexpr uint32_t BUF_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, bool on = true) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, on ? 0x7FFFFFFF : 0, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     if (nwg <= 8) return orig;
     const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;

@@ -55,7 +55,7 @@ __device__ __forceinline__ void unpack8(const u32x4 w, float (&v)[8]) {
     }
 }
 
-template <int W, int R, int EPI>  // EPI 0: forward (+ shifted BN statistics), 1: fused BN backward
+template <int W, int R, int EPI>  // EPI 0: forward (+ shifted BN statistics), 1: fused BN backward, 2: + second BN branch
 __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int nbands) {
     constexpr int PW = halo_pw(W);
     constexpr int PCOLS = W + 2, PROWS = R + 2;
@@ -99,24 +99,17 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
     }
     u32x4 pr[PMAX];
     bool pv[PMAX];  // chunk inside the image (xbn: transformed at staging)
-    auto load_patch = [&](int band) {
+    auto load_patch = [&](int band) {  // branch-free: out-of-image chunks are out-of-range buffer offsets (zeros)
         const int img = band / bands_per_img, y0 = (band - img * bands_per_img) * R;
-        const bf16_t* xi = a.X + (size_t)img * a.H * W * 64;
+        const __amdgpu_buffer_rsrc_t rxi = buf_rsrc(a.X + (size_t)img * a.H * W * 64);
 #pragma unroll
         for (int i = 0; i < PMAX; ++i) {
             const int id = tid + i * 512;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            pv[i] = false;
-            if (id < NCH) {
-                const int c = id & 7, pix = id >> 3;
-                const int prow = pix / PCOLS, pcol = pix - prow * PCOLS;
-                const int iy = y0 - 1 + prow, ix = pcol - 1;
-                if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)W) {
-                    v = *reinterpret_cast<const u32x4*>(xi + ((size_t)iy * W + ix) * 64 + c * 8);
-                    pv[i] = true;
-                }
-            }
-            pr[i] = v;
+            const int c = id & 7, pix = id >> 3;
+            const int prow = pix / PCOLS, pcol = pix - prow * PCOLS;
+            const int iy = y0 - 1 + prow, ix = pcol - 1;
+            pv[i] = id < NCH && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)W;
+            pr[i] = buf_ld16(rxi, pv[i] ? (uint32_t)(((iy * W + ix) * 64 + c * 8) * 2) : BUF_OOB);
         }
     };
     auto store_patch = [&]() {
@@ -157,7 +150,8 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
     const bool want_st = a.stats != nullptr;
     const bool accum = a.flags & IG_ACCUM;
     const bool affine = a.flags & IG_AFFINE, relu = a.flags & IG_RELU;  // eval forward (EPI 0 only)
-    const bool has_y = EPI == 1 && a.bnym != nullptr, has_x2 = EPI == 1 && a.bnx2 != nullptr;
+    const bool has_y = EPI >= 1 && a.bnym != nullptr;
+    constexpr bool has_x2 = EPI == 2;
     float c0[8], c1[8], c2[8], c3[8];  // per-channel constants (see below)
     float s1[8], s2[8], s3[8];
 #pragma unroll
@@ -190,7 +184,28 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         __syncthreads();  // previous patch / staging reads done (and the weights are in)
         store_patch();
         __syncthreads();
-        if (b + 1 < b1) load_patch(b + 1);  // in flight while this band computes
+        // the epilogue's global operands of THIS band go out before the next band's patch loads: vmcnt retires
+        // in issue order, so the epilogue's wait for them leaves the patch prefetch in flight
+        const int img = b / bands_per_img, y0 = (b - img * bands_per_img) * R;
+        const size_t m0 = (size_t)(img * a.H + y0) * W;
+        const __amdgpu_buffer_rsrc_t ry = buf_rsrc(reinterpret_cast<const bf16_t*>(a.Y) + m0 * 64);
+        // (x and the mask bits of the BN-backward epilogue at W = 56; the rarer accumulated output, the second
+        // branch's x (EPI 2) and the 112-wide band read in the epilogue itself: up front they spill at 256 VGPRs)
+        constexpr bool PRE = EPI == 1 && W == 56;
+        u32x4 xw[4];
+        uint32_t yw[4];
+        const __amdgpu_buffer_rsrc_t rx2 = buf_rsrc(a.bnx2 + m0 * 64, has_x2);
+        const __amdgpu_buffer_rsrc_t rbx = buf_rsrc(a.bnx + m0 * 64, EPI >= 1);
+        const __amdgpu_buffer_rsrc_t rym = buf_rsrc(a.bnym + m0 * 8, has_y);
+        if (PRE && active) {
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+                const uint32_t off = (uint32_t)(((ep0 + 8 * k4) * 64 + ec * 8) * 2);
+                xw[k4] = buf_ld16(rbx, off);
+                yw[k4] = has_y ? __builtin_amdgcn_raw_buffer_load_b8(rym, off >> 4, 0, 0) : 0u;
+            }
+        }
+        load_patch(b + 1 < b1 ? b + 1 : b);  // in flight while this band computes (the last band re-reads itself)
         if (active) {
             f32x4 acc[4][2];
 #pragma unroll
@@ -239,39 +254,38 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // coalesced epilogue: the band's output pixels are contiguous in NHWC
-        const int img = b / bands_per_img, y0 = (b - img * bands_per_img) * R;
-        const size_t m0 = (size_t)(img * a.H + y0) * W;
-#pragma unroll 1
+        constexpr int EU = PRE ? 4 : 1;  // register arrays need the unrolled loop; the late-load form stays rolled
+#pragma unroll EU
         for (int k4 = 0; k4 < 4; ++k4) {
             const int p = ep0 + 8 * k4;
-            const size_t e = (m0 + p) * 64 + ec * 8;
+            const uint32_t off = (uint32_t)((p * 64 + ec * 8) * 2);
             float v[8];
             unpack8(*reinterpret_cast<const u32x4*>(sE + p * HALO_SP + ec * 16), v);
-            bf16_t* yp = reinterpret_cast<bf16_t*>(a.Y) + e;
-            u32x4 xw = {0u, 0u, 0u, 0u}, x2w = xw, ow = xw;
-            uint32_t yw = 0u;
-            if (accum) ow = *reinterpret_cast<const u32x4*>(yp);
             if (EPI == 0 && affine) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) v[q] = fmaf(v[q], c2[q], c3[q]);
             }
-            if (EPI == 1) {
-                xw = *reinterpret_cast<const u32x4*>(a.bnx + e);
-                if (has_y) yw = a.bnym[e >> 3];
-                if (has_x2) x2w = *reinterpret_cast<const u32x4*>(a.bnx2 + e);
-            }
             if (accum) {
                 float o[8];
-                unpack8(ow, o);
+                unpack8(buf_ld16(ry, off), o);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) v[q] += o[q];
             }
-            if (EPI == 1) {
+            if (EPI >= 1) {
+                u32x4 xk;
+                uint32_t yk;
+                if constexpr (PRE) {
+                    xk = xw[k4];
+                    yk = yw[k4];
+                } else {
+                    xk = buf_ld16(rbx, off);
+                    yk = has_y ? __builtin_amdgcn_raw_buffer_load_b8(rym, off >> 4, 0, 0) : 0u;
+                }
                 float xv[8], mk[8];
-                unpack8(xw, xv);
+                unpack8(xk, xv);
                 if (has_y) {
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) mk[q] = (yw >> q) & 1u ? 1.f : 0.f;
+                    for (int q = 0; q < 8; ++q) mk[q] = (yk >> q) & 1u ? 1.f : 0.f;
                 } else {
 #pragma unroll
                     for (int q = 0; q < 8; ++q) mk[q] = fmaf(xv[q], c2[q], c3[q]);
@@ -282,10 +296,10 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                 u32x4 out;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) out[q] = pack_bf2(v[2 * q], v[2 * q + 1]);
-                *reinterpret_cast<u32x4*>(yp) = out;
+                buf_st16(ry, off, out);
                 unpack8(out, v);
                 float x2v[8];
-                if (has_x2) unpack8(x2w, x2v);
+                if (has_x2) unpack8(buf_ld16(rx2, off), x2v);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     s1[q] += v[q] * ((xv[q] - c0[q]) * c1[q]);  // sum g * xhat
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
                 u32x4 out;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) out[q] = pack_bf2(v[2 * q], v[2 * q + 1]);
-                *reinterpret_cast<u32x4*>(yp) = out;
+                buf_st16(ry, off, out);
                 if (want_st) {
                     unpack8(out, v);
 #pragma unroll
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(512, 1) void halo3x3_kernel(const IGemmArgs a, int 
         const int qq = tid >> 6, n = tid & 63, c = n >> 3, k = n & 7;
         float sum = 0.f;
         for (int u = c; u < 512; u += 8) sum += red[(qq * 512 + u) * 8 + k];
-        float* st = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * (EPI == 1 ? 3 : 2) * a.Nout;
+        float* st = a.stats + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * (EPI >= 1 ? 3 : 2) * a.Nout;
         atomicAdd(st + qq * a.Nout + n, sum);
     }
 }
@@ -379,8 +393,9 @@ int conv_halo(const IGemmArgs& a, hipStream_t st) {
     const bool bnb = a.flags & IG_BNBWD;
     if (bnb && a.bnx2 && !a.bnym) return 1;  // a second BN branch needs the output's mask bits (c2/c3 hold its constants)
     if (a.W == 56 && a.H % 4 == 0)
-        return bnb ? launch_halo<56, 4, 1>(a, st) : launch_halo<56, 4, 0>(a, st);
+        return bnb ? (a.bnx2 ? launch_halo<56, 4, 2>(a, st) : launch_halo<56, 4, 1>(a, st)) : launch_halo<56, 4, 0>(a, st);
     if (a.W == 112 && a.H % 2 == 0)
-        return bnb ? launch_halo<112, 2, 1>(a, st) : launch_halo<112, 2, 0>(a, st);
+        return bnb ? (a.bnx2 ? launch_halo<112, 2, 2>(a, st) : launch_halo<112, 2, 1>(a, st))
+                   : launch_halo<112, 2, 0>(a, st);
     return 1;
 }

@@ -43,16 +43,6 @@
 
 namespace {
 
-// raw buffer access of the streaming loop: num_records 2^31 - 1, or 0 for an operand the launch does not use
-// (its loads read zeros, its stores are dropped); per-lane offsets >= SOOB are out of range (rows past M)
-constexpr uint32_t SOOB = 0x80000000u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t s_rsrc(const void* p, bool on) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, on ? 0x7FFFFFFF : 0, 0x00020000);
-}
-__device__ __forceinline__ u32x4 s_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-}
-
 // MODE 0: plain epilogue (+ optional IG_ACCUM); IG_BNBWD with the ReLU mask
 // from the saved output y (1), recomputed from x (2), y + second BN branch x2 (3); 4: the plain epilogue with
 // a training block's fused output (IG_RES residual (+ scale), IG_MASKOUT mask bits, IG_Q8OUT e4m3 copy) -- a
@@ -217,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             const int oh = rem / a.OW, ow = rem - oh * a.OW;
             row0 = ((size_t)img * a.H + oh * a.sA) * a.W + ow * a.sA;
         }
-        uint32_t off = SOOB;
+        uint32_t off = BUF_OOB;
         if (ok) {
             size_t row = (size_t)m;
             if (!dense) {
@@ -227,18 +217,74 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
             off = (uint32_t)((row - row0) * a.C * 2) + fq * 16;
         }
-        const __amdgpu_buffer_rsrc_t rx = s_rsrc(a.X + row0 * a.C, true);
+        const __amdgpu_buffer_rsrc_t rx = buf_rsrc(a.X + row0 * a.C, true);
 #pragma unroll
-        for (int ks = 0; ks < KS1; ++ks) pf[d][ks] = s_ld16(rx, off + ks * 64);
+        for (int ks = 0; ks < KS1; ++ks) pf[d][ks] = buf_ld16(rx, off + ks * 64);
         if constexpr (K2 > 0) {  // (dense rows only: host check)
-            const __amdgpu_buffer_rsrc_t rx2 = s_rsrc(a.X2 + (size_t)m0 * K2, true);
-            const uint32_t off2 = ok ? (uint32_t)(fr * K2 * 2 + fq * 16) : SOOB;
+            const __amdgpu_buffer_rsrc_t rx2 = buf_rsrc(a.X2 + (size_t)m0 * K2, true);
+            const uint32_t off2 = ok ? (uint32_t)(fr * K2 * 2 + fq * 16) : BUF_OOB;
 #pragma unroll
-            for (int ks = KS1; ks < KS; ++ks) pf[d][ks] = s_ld16(rx2, off2 + (ks - KS1) * 64);
+            for (int ks = KS1; ks < KS; ++ks) pf[d][ks] = buf_ld16(rx2, off2 + (ks - KS1) * 64);
+        }
+    };
+    // epilogue operand addressing of group g
+    struct EpiBase {
+        __amdgpu_buffer_rsrc_t ry, ro, rbx, rx2o, rym, ry8;
+    };
+    auto epi_base = [&](int g) {
+        const size_t eb0 = (size_t)(g < ngroups ? g * 16 : 0) * a.ldy;
+        const bf16_t* ybase = reinterpret_cast<const bf16_t*>(a.Y) + eb0;
+        EpiBase e;
+        e.ry = buf_rsrc(ybase, true);
+        e.ro = buf_rsrc(accum ? ybase : a.bnx + eb0, accum || resid);
+        e.rbx = buf_rsrc(a.bnx + eb0, bnb && a.bnx);  // bnx null (mask bits given): x is never read (zeros)
+        e.rx2o = buf_rsrc(a.bnx2 + eb0, has_x2);
+        e.rym = buf_rsrc(a.bnym + eb0 / 8, has_y || maskout);
+        e.ry8 = buf_rsrc(reinterpret_cast<const uint8_t*>(a.Y8) + eb0, q8out);
+        return e;
+    };
+    auto epi_off = [&](int g, int u, bool& ev, uint32_t& o2) {  // row u * PPR + lane / CH of group g, channels n..
+        const int pr = u * PPR + lane / CH;
+        ev = g < ngroups && g * 16 + pr < a.M;
+        o2 = ev ? (uint32_t)(pr * a.ldy + n) * 2 : BUF_OOB;  // bytes from the group's base
+    };
+    auto oo_off = [&](int g, int u, uint32_t o2) {
+        if (accum && (a.flags & IG_ACCUM_SUB2)) {  // dense output grid: only even (oh, ow) accumulate
+            const int rem = (g * 16 + u * PPR + lane / CH) % ohw, oh = rem / a.OW;
+            if (((oh | (rem - oh * a.OW)) & 1) != 0) return BUF_OOB;
+        }
+        return o2;
+    };
+    // EPF: the epilogue's global operands (residual / BN-backward x, mask bits, second-branch x) are prefetched D
+    // groups ahead, as the pixel operand is: issued at the start of their own group they left one memory latency
+    // exposed per group (<256, 64> fused output at 14x14: 3.5 us per group and wave for 32 MFMAs). Kept where
+    // the registers allow (no spill at 256 VGPRs)
+    constexpr bool early = bnb || FO;
+    constexpr int EPR = FO ? 4 : bnb ? 4 + (has_y ? 1 : 0) + (has_x2 ? 4 : 0) : 0;  // VGPRs per row chunk
+    constexpr bool EPF = early && !STEM && !XBN && D * NR * EPR <= 32;
+    u32x4 eoo[EPF ? D : 1][NR], exo[EPF ? D : 1][NR], ex2o[EPF ? D : 1][NR];
+    uint32_t eyo[EPF ? D : 1][NR];
+    auto issue_early = [&](int d, int g) {
+        const EpiBase e = epi_base(g);
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            bool ev;
+            uint32_t o2;
+            epi_off(g, u, ev, o2);
+            eoo[d][u] = buf_ld16(e.ro, oo_off(g, u, o2));
+            if (bnb) {
+                exo[d][u] = buf_ld16(e.rbx, o2);
+                if (has_y) eyo[d][u] = __builtin_amdgcn_raw_buffer_load_b8(e.rym, ev ? o2 >> 4 : BUF_OOB, 0, 0);
+                if (has_x2) ex2o[d][u] = buf_ld16(e.rx2o, o2);
+            }
         }
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) fetch(d, w0 + d * wstride);
+    if constexpr (EPF) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) issue_early(d, w0 + d * wstride);
+    }
     __syncthreads();  // weight slice visible
 
     int aoff[KS];
@@ -280,44 +326,35 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
             }
             // the group's epilogue operands: wave-uniform bases at the group's pixel row, per-lane byte offsets
             // (rows past M: out of range, loads read zeros and stores are dropped). Every load of the loop body is
-            // unconditional, so the prefetch below stays in flight through the epilogue's waits
-            const size_t eb0 = (size_t)(g < ngroups ? g * 16 : 0) * a.ldy;
-            const bf16_t* ybase = reinterpret_cast<const bf16_t*>(a.Y) + eb0;
-            const __amdgpu_buffer_rsrc_t ry = s_rsrc(ybase, true);
-            const __amdgpu_buffer_rsrc_t ro = s_rsrc(accum ? ybase : a.bnx + eb0, accum || resid);
-            const __amdgpu_buffer_rsrc_t rbx = s_rsrc(a.bnx + eb0, bnb && a.bnx);
-            const __amdgpu_buffer_rsrc_t rx2o = s_rsrc(a.bnx2 + eb0, has_x2);
-            const __amdgpu_buffer_rsrc_t rym = s_rsrc(a.bnym + eb0 / 8, has_y || maskout);
-            const __amdgpu_buffer_rsrc_t ry8 = s_rsrc(reinterpret_cast<const uint8_t*>(a.Y8) + eb0, q8out);
-            constexpr bool early = bnb || FO;
+            // unconditional, so the waits stay counted and the prefetch stays in flight
+            const EpiBase eb = epi_base(g);
             bool ev[NR];
             uint32_t o2[NR];
             u32x4 oo[NR], xo[NR], x2o[NR];
             uint32_t yo[NR];
-            auto issue = [&](int u) {
-                const int pr = u * PPR + lane / CH;
-                const int m = g * 16 + pr;
-                ev[u] = g < ngroups && m < a.M;
-                const uint32_t rel = (uint32_t)(pr * a.ldy + n);  // elements from eb0
-                o2[u] = ev[u] ? rel * 2 : SOOB;
-                uint32_t oo_off = o2[u];
-                if (accum && (a.flags & IG_ACCUM_SUB2)) {  // dense output grid: only even (oh, ow) accumulate
-                    const int rem = m % ohw, oh = rem / a.OW;
-                    if (((oh | (rem - oh * a.OW)) & 1) != 0) oo_off = SOOB;
-                }
-                if (early || accum) oo[u] = s_ld16(ro, oo_off);  // (plain mode: a uniform branch, late in the epilogue)
+#pragma unroll
+            for (int u = 0; u < NR; ++u) epi_off(g, u, ev[u], o2[u]);
+            auto issue = [&](int u) {  // late / at-group-start form of the epilogue operand loads
+                if (early || accum) oo[u] = buf_ld16(eb.ro, oo_off(g, u, o2[u]));
                 if (bnb) {
-                    // bnx null (mask bits given): slot 0 of the slab is then not sum(g xhat) (bn_gram.hip forms
-                    // it from g^T h2) and x is never read (zeros)
-                    xo[u] = s_ld16(rbx, o2[u]);
-                    if (has_y) yo[u] = __builtin_amdgcn_raw_buffer_load_b8(rym, ev[u] ? rel >> 3 : SOOB, 0, 0);
-                    if (has_x2) x2o[u] = s_ld16(rx2o, o2[u]);
+                    xo[u] = buf_ld16(eb.rbx, o2[u]);
+                    if (has_y) yo[u] = __builtin_amdgcn_raw_buffer_load_b8(eb.rym, ev[u] ? o2[u] >> 4 : BUF_OOB, 0, 0);
+                    if (has_x2) x2o[u] = buf_ld16(eb.rx2o, o2[u]);
                 }
             };
-            // the BN-backward (x / mask) and residual reads go out before the MFMAs and BEFORE the next prefetch:
-            // waiting for them leaves the prefetch in flight (the accumulated old output of the plain mode is read
-            // in the epilogue: issued early it measured slower, eval 52.8k -> 48.9k val img/s)
-            if constexpr (early) {
+            if constexpr (EPF) {  // issued D groups ago (below): take them over
+#pragma unroll
+                for (int u = 0; u < NR; ++u) {
+                    oo[u] = eoo[d][u];
+                    if (bnb) {
+                        xo[u] = exo[d][u];
+                        if (has_y) yo[u] = eyo[d][u];
+                        if (has_x2) x2o[u] = ex2o[d][u];
+                    }
+                }
+            } else if constexpr (early) {
+                // the BN-backward (x / mask) and residual reads go out before the MFMAs and BEFORE the next
+                // prefetch: waiting for them leaves the prefetch in flight
 #pragma unroll
                 for (int u = 0; u < NR; ++u) issue(u);
             }
@@ -407,7 +444,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                     u32x4 o;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) o[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
-                    __builtin_amdgcn_raw_buffer_store_b128(o, ry, o2[q], 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(o, eb.ry, o2[q], 0, 0);
                     if (q8out) {  // quantise the bf16-rounded values the bf16 consumers see
                         float w[8];
 #pragma unroll
@@ -420,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                         __builtin_amdgcn_raw_buffer_store_b64(
                             u32x2{pack4_fp8(w[0] * q8s, w[1] * q8s, w[2] * q8s, w[3] * q8s),
                                   pack4_fp8(w[4] * q8s, w[5] * q8s, w[6] * q8s, w[7] * q8s)},
-                            ry8, ev[q] ? o2[q] / 2 : SOOB, 0, 0);
+                            eb.ry8, ev[q] ? o2[q] / 2 : BUF_OOB, 0, 0);
                     }
                     if (maskout) {  // stored bf16 > 0: nonzero, sign clear, not NaN (as bn_fwd's ym)
                         uint32_t b = 0;
@@ -429,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                             const uint32_t h = (o[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
                             b |= (h != 0u && h <= 0x7F80u ? 1u : 0u) << i;
                         }
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rym, ev[q] ? o2[q] / 16 : SOOB, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, eb.rym, ev[q] ? o2[q] / 16 : BUF_OOB, 0, 0);
                     }
                     if (a.stats) {
 #pragma unroll
@@ -462,6 +499,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            if constexpr (EPF) issue_early(d, g + D * wstride);
         }
     }
     if (q8out) {  // one atomic per wave into the 32-slot amax row
@@ -719,6 +757,7 @@ int conv_stem(const IGemmArgs& a, hipStream_t st, int tile) {
 // Returns 1 if the shape is not one this kernel covers (caller falls back).
 // bn: channel-slice width (0 auto: the widest that divides Nout; 64/128/256 forced)
 int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
+    const int bn_hint = bn;  // explicit slice width (tiles 20-22), before the defaults below
     // the eval forward's folded BatchNorm (+ ReLU): plain epilogue, no statistics
     const bool eval_bn = a.flags & IG_AFFINE;
     if ((a.flags & IG_RELU) && !eval_bn) return 1;
@@ -771,6 +810,7 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // 512 -> 1024 /2 @28 443 -> 375, 2048 -> 512 dgrad 209 -> 152; K = 256 stays here: 256 -> 1024 @14
     // fwd 264 vs 370).
     if (!(a.flags & IG_BNBWD) && a.C == 256 && a.Nout > 128) {
+        if (bn == 128 && a.Nout % 128 == 0) return launch_plain<256, 128, 2>(a, st);  // (tile 21: A/B)
         if (bn != 0 && bn != 64) return 1;
         return launch_plain<256, 64, 2>(a, st);
     }
@@ -799,6 +839,8 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // weight slices resident in LDS (as the K = 256 forwards) instead of the one-tile-per-block v3 loop, whose
     // 4-stage main loop leaves these epilogue-heavy GEMMs latency-bound (-20 % per call, round 4)
     if (a.C == 256 && (a.flags & IG_BNBWD) && a.Nout > 128) {
+        if (bn_hint == 128 && !a.bnx2 && a.Nout % 128 == 0)  // (tile 21: A/B)
+            return a.bnym ? launch_stream1<256, 128, 2, 1>(a, st) : launch_stream1<256, 128, 2, 2>(a, st);
         if (a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 3>(a, st) : 1;
         return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);
     }

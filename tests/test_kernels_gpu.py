@@ -748,3 +748,49 @@ def test_halo_conv3x3(shape):
     assert rel(dx.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
+
+
+@pytest.mark.parametrize("variant", ["y_mask", "x_mask", "x2"])
+@pytest.mark.parametrize("N,H", [(3, 56), (2, 112)])
+def test_halo_dgrad_bnb_matches_tiled(N, H, variant):
+    """The halo kernel's fused BatchNorm-backward dgrad epilogue (EPI 1: x / mask-bit operands prefetched before the
+    next band's patch at W = 56; EPI 2: the second BN branch) against the tiled kernel (tile 1) on the same
+    operands: stored gradient and the three slab reductions."""
+    from imagent_amd.models.resnet import BatchNorm2d, BNWork
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.bn import relu_mask_bits
+    from imagent_amd.ops.conv import BNBwdFuse, igemm_dgrad
+    from torch.profiler import ProfilerActivity, profile
+    C = 64
+    torch.manual_seed(11)
+    dy = bf(torch.randn(N, H, H, C, device=DEV))
+    wt = bf(torch.randn(C, 3, 3, C, device=DEV) * (1.0 / (9 * C)) ** 0.5)
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    y = bf(torch.randn(N, H, H, C, device=DEV)) if variant in ("y_mask", "x2") else None
+    x2 = bf(torch.randn(N, H, H, C, device=DEV)) if variant == "x2" else None
+    nbw = _lib.kernels().imk_bn_bwd_scratch_floats(1)
+
+    def mk():
+        bn = BatchNorm2d(C).to(DEV)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+        save = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5])
+        bn.work = BNWork(None, None, save, torch.zeros(nbw * C, device=DEV))
+        return bn
+
+    bn, bn2 = mk(), mk()
+    outs = []
+    for tile in (0, 1):
+        bn.work.scratch.zero_()
+        f = BNBwdFuse(x, bn, y=relu_mask_bits(y) if y is not None else None, x2=x2, bn2=bn2 if x2 is not None else None)
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            r = igemm_dgrad(dy, wt, (H, H), 1, 1, 3, 3, bnb=f, tile=tile)
+            torch.cuda.synchronize()
+        halo = any("halo3x3_kernel" in e.name for e in prof.events())
+        assert halo == (tile == 0), tile
+        outs.append((r.clone(), bn.work.scratch[:32 * 3 * C].view(32, 3, C).sum(0).clone()))
+    (r0, s0), (r1, s1) = outs
+    assert rel(r0, r1) < 5e-3
+    for q in range(3 if x2 is not None else 2):
+        assert rel(s0[q], s1[q]) < 2e-3, q
