@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const IGemmArgs a) 
     // the registers allow (no spill at 256 VGPRs)
     constexpr bool early = bnb || FO;
     constexpr int EPR = FO ? 4 : bnb ? 4 + (has_y ? 1 : 0) + (has_x2 ? 4 : 0) : 0;  // VGPRs per row chunk
-    constexpr bool EPF = early && !STEM && !XBN && D * NR * EPR <= 32;
+    constexpr bool EPF = early && !STEM && !XBN && D * NR * EPR <= (K >= 256 && BN >= 128 ? 16 : 32);
     u32x4 eoo[EPF ? D : 1][NR], exo[EPF ? D : 1][NR], ex2o[EPF ? D : 1][NR];
     uint32_t eyo[EPF ? D : 1][NR];
     auto issue_early = [&](int d, int g) {
@@ -809,8 +809,10 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // Only K = 256: at K = 512 the v3 tiles win (conv_bench at 1024 img: 512 -> 2048 @7 fwd 210 -> 179 us,
     // 512 -> 1024 /2 @28 443 -> 375, 2048 -> 512 dgrad 209 -> 152; K = 256 stays here: 256 -> 1024 @14
     // fwd 264 vs 370).
+    // 128-channel slices where Nout allows (half the slices re-reading each pixel group, twice the MFMAs per
+    // loaded fragment: 256 -> 1024 @14 fwd 277 -> 246 us at 1024 img, round 5); tile 22 forces 64
     if (!(a.flags & IG_BNBWD) && a.C == 256 && a.Nout > 128) {
-        if (bn == 128 && a.Nout % 128 == 0) return launch_plain<256, 128, 2>(a, st);  // (tile 21: A/B)
+        if (bn != 64 && a.Nout % 128 == 0) return launch_plain<256, 128, 2>(a, st);
         if (bn != 0 && bn != 64) return 1;
         return launch_plain<256, 64, 2>(a, st);
     }
