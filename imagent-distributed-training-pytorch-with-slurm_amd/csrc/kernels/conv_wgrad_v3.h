@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wco = wid & 1, wkc = wid >> 1;
     const int K = a.KH * a.KW * a.Ci;
-    const int nco = a.Co / 128, nkc = (K + 127) / 128;  // (K = 64: one half-used k tile, see wgrad_v3_ok)
+    const int nco = (a.Co + 127) / 128, nkc = (K + 127) / 128;  // (Co / K = 64: one half-used tile, wgrad_v3_ok)
     const int ntiles = nco * nkc;
     const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tile = lid % ntiles, split = lid / ntiles;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
         const int buf = s % NS;
         const char* bD = sD + buf * SB;
         const char* bX = sX + buf * SB;
-        if (kc0 + wkc * 64 >= K) continue;  // (wave-uniform) columns past K: staged, never computed
+        if (kc0 + wkc * 64 >= K || co0 + wco * 64 >= a.Co) continue;  // (wave-uniform) past K / Co: never computed
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             bf16x8 fd[4], fx[4];
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
     }
 
     // acc[i][j][r]: co = co0 + wco*64 + i*16 + (lane>>4)*4 + r ; k = kc0 + wkc*64 + j*16 + (lane&15)
-    if (kc0 + wkc * 64 >= K) return;
+    if (kc0 + wkc * 64 >= K || co0 + wco * 64 >= a.Co) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -192,7 +192,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
 // one k tile whose 256-B X rows span two pixels -- the second pixel's 64 channels land in columns 64..127, which
 // the waves owning them skip (no MFMA, no store); the last row's overhang reads zeros past the descriptor's range
 bool wgrad_v3_ok(const WgradArgs& a) {
-    if (a.stem || a.xbn || a.Co % 128) return false;
+    if (a.stem || a.xbn) return false;
+    if (a.Co % 128 && !(a.Co == 64 && a.KH == 1 && a.KW == 1)) return false;  // (Co = 64: the same, on dY's rows)
     if (a.Ci % 128 && !(a.Ci == 64 && a.KH == 1 && a.KW == 1)) return false;
     if ((size_t)a.M * a.Co * 2 >= (1u << 31) || (size_t)a.N * a.H * a.W * a.Ci * 2 >= (1u << 31)) return false;
     return true;
@@ -201,7 +202,7 @@ bool wgrad_v3_ok(const WgradArgs& a) {
 template <int BR, int NS>
 int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
     const int K = a.KH * a.KW * a.Ci;
-    const int ntiles = (a.Co / 128) * ((K + 127) / 128);
+    const int ntiles = ((a.Co + 127) / 128) * ((K + 127) / 128);
     if (splits <= 0) {
         // one wave of 2 blocks per CU over 256 CUs: the 1x1 wgrads are split-K streams whose second, partial
         // wave of blocks cost more than the extra atomics of deeper splits save (same-box bench: 512 blocks

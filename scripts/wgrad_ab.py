@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # (Ci, H, Co, k, s, calls per step at R50)
 SHAPES = [(128, 56, 128, 3, 2, 1), (256, 28, 256, 3, 2, 1), (512, 14, 512, 3, 2, 1), (512, 7, 512, 3, 1, 2),
-          (64, 56, 256, 1, 1, 4), (64, 56, 64, 1, 1, 1), (64, 56, 64, 3, 1, 3), (128, 28, 128, 3, 1, 3)]
+          (64, 56, 256, 1, 1, 4), (64, 56, 64, 1, 1, 1), (256, 56, 64, 1, 1, 2), (64, 56, 64, 3, 1, 3), (128, 28, 128, 3, 1, 3)]
 
 
 def main():

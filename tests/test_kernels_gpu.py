@@ -192,9 +192,10 @@ def test_wgrad_variants(shape, splits):
 @pytest.mark.parametrize("variant", [-1, 1, 2, 3, 4])
 @pytest.mark.parametrize("shape", [(4, 128, 14, 128, 3, 1, 1), (3, 256, 9, 128, 3, 2, 1), (2, 128, 7, 256, 3, 1, 1),
                                    (3, 256, 11, 384, 1, 1, 0), (2, 128, 10, 256, 1, 2, 0), (1, 128, 5, 128, 3, 1, 1),
-                                   (3, 64, 13, 256, 1, 1, 0), (2, 64, 10, 128, 1, 2, 0)])
+                                   (3, 64, 13, 256, 1, 1, 0), (2, 64, 10, 128, 1, 2, 0), (3, 256, 9, 64, 1, 1, 0),
+                                   (2, 64, 11, 64, 1, 1, 0)])
 def test_wgrad_v3(shape, variant):
-    """LDS-DMA weight gradient (conv_wgrad_v3.h, Ci % 128 == 0 or a Ci = 64 1x1, Co % 128 == 0) and the
+    """LDS-DMA weight gradient (conv_wgrad_v3.h, Ci and Co % 128 == 0, or 64 on a 1x1) and the
     register-staged kernel on the same shapes: 3x3 stride 1 / 2 with image borders, 1x1 dense and strided
     (Ci = 64: one half-used k tile), an M that is not a multiple of the stage rows, explicit split-K."""
     from imagent_amd.ops.conv import igemm_wgrad
