@@ -90,10 +90,17 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
     const int ohw = a.OH * a.OW;
     const int lrow = lane / CPR;
     const int lchunk = (lane % CPR) ^ lds_swz<RB>(lrow);
-    const __amdgpu_buffer_rsrc_t rx = v3_rsrc(a.X, (uint32_t)((size_t)a.N * a.H * a.W * a.C * EB));
+    // descriptors based at the tile's first image (X) / first pixel row (X2): a tile's rows span a few images at
+    // most, so the 32-bit buffer offsets hold for any tensor size (batch 2048 puts 3.3 GB in one layer-1 tensor)
+    const int img0 = m0 / ohw;
+    const size_t xo0 = (size_t)img0 * a.H * a.W * a.C * EB, xall = (size_t)a.N * a.H * a.W * a.C * EB;
+    const __amdgpu_buffer_rsrc_t rx =
+        v3_rsrc(reinterpret_cast<const char*>(a.X) + xo0, (uint32_t)min(xall - xo0, (size_t)0x7FFFFFFF));
     const __amdgpu_buffer_rsrc_t rw = v3_rsrc(a.Wk, (uint32_t)((size_t)a.Nout * a.ldb * EB));
+    const size_t x2o0 = (size_t)m0 * a.C2 * 2;
     const __amdgpu_buffer_rsrc_t rx2 =
-        v3_rsrc(a.X2 ? a.X2 : a.X, a.X2 ? (uint32_t)((size_t)a.M * a.C2 * 2) : 0u);
+        v3_rsrc(a.X2 ? reinterpret_cast<const char*>(a.X2) + x2o0 : reinterpret_cast<const char*>(a.X),
+                a.X2 ? (uint32_t)min((size_t)a.M * a.C2 * 2 - x2o0, (size_t)0x7FFFFFFF) : 0u);
 
     // per X piece: byte offset of (img, ih0, iw0, lchunk) -- may be "negative" (a border pixel's
     // first tap), only valid taps' offsets are ever used -- and the valid-tap bit mask
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
         const int img = mm / ohw, rem = mm - img * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         const int ih0 = oh * a.sA + a.dh0, iw0 = ow * a.sA + a.dw0;
-        xbase[q] = (((int64_t)img * a.H + ih0) * a.W + iw0) * a.C * EB + lchunk * 16;
+        xbase[q] = (((int64_t)(img - img0) * a.H + ih0) * a.W + iw0) * a.C * EB + lchunk * 16;
         uint32_t mk = 0;
         for (int ti = 0; ti < a.nth; ++ti) {
             const int ih = ih0 + ti * a.dhs;
@@ -122,7 +129,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void igemm_v3_kernel(cons
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
         const int m = m0 + (wid * QA + q) * RPP + lrow;
-        xbase2[q] = m < a.M ? (uint32_t)((size_t)m * a.C2 * 2 + lchunk * 16) : OOB_OFF;
+        xbase2[q] = m < a.M ? (uint32_t)((size_t)(m - m0) * a.C2 * 2 + lchunk * 16) : OOB_OFF;
     }
     uint32_t vw[QB];
 #pragma unroll
@@ -417,10 +424,11 @@ inline bool v3_ok(const IGemmArgs& a) {
     const bool bnb_bias = (a.flags & IG_BNBWD) && a.X2;  // the second segment's bias (bn_gram.hip)
     if ((a.bias && !eval_bn && !bnb_bias) || a.xbn || a.Nout % 8 || a.ldy % 8) return false;
     if (a.X2 && (a.C2 % 64 || a.C2 <= 0 || a.nth != 1 || a.ntw != 1 || a.sA != 1 || a.H != a.OH || a.W != a.OW ||
-                 a.ldb < a.C + a.C2 || (size_t)a.M * a.C2 * 2 >= (1ull << 31)))
+                 a.ldb < a.C + a.C2))
         return false;
-    const size_t xb = (size_t)a.N * a.H * a.W * a.C * 2, wb = (size_t)a.Nout * a.ldb * 2;
-    return xb < (1ull << 31) && wb < (1ull << 31);
+    // (X / X2 descriptors are tile-based: any size; one image must stay below 2^31 bytes, the weights too)
+    const size_t ib = (size_t)a.H * a.W * a.C * 2 * 4, wb = (size_t)a.Nout * a.ldb * 2;
+    return ib < (1ull << 31) && wb < (1ull << 31);
 }
 
 // fp32 (3 x bf16 split, EB = 4) shapes v3 covers: C % 32 == 0 (one tap per 32-deep stage), fp32 out with

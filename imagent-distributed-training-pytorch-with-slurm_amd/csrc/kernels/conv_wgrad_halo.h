@@ -72,17 +72,20 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
     if (b0 >= b1) return;  // whole block
     const int bpi = a.OH / R;
     const uint32_t ldy = (uint32_t)a.Co * 2, ldx = (uint32_t)a.Ci * 2;  // pixel pitches, bytes
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(a.dY + co0), (short)0, (int)((size_t)a.M * ldy - co0 * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(a.X + ci0), (short)0, (int)((size_t)a.N * a.H * a.W * ldx - ci0 * 2), 0x00020000);
+    // descriptors based at the band's image (issue_band): 32-bit offsets for any batch size
+    const size_t dall = (size_t)a.M * a.Co, xall = (size_t)a.N * a.H * a.W * a.Ci;
 
     // ---- DMA of band `band` into buffer `buf`: piece k of this wave = LDS rows 8k' .. 8k' + 7,
     // lane -> (row (lane >> 3), slot lane & 7), source chunk = slot's logical chunk
     const int drow = lane >> 3, dslot = lane & 7;
     auto issue_band = [&](int band, int buf) {
         const int img = band / bpi, y0 = (band - img * bpi) * R;
-        const uint32_t pix0 = (uint32_t)((img * a.OH + y0) * W);  // band's first (output) pixel
+        const uint32_t pix0 = (uint32_t)(y0 * W);  // band's first (output) pixel within its image
+        const size_t dimg = (size_t)img * a.OH * W * a.Co + co0, ximg = (size_t)img * a.H * a.W * a.Ci + ci0;
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<bf16_t*>(a.dY + dimg), (short)0, (int)min((dall - dimg) * 2, (size_t)0x7FFFFFFF), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<bf16_t*>(a.X + ximg), (short)0, (int)min((xall - ximg) * 2, (size_t)0x7FFFFFFF), 0x00020000);
 #pragma unroll
         for (int k = 0; k < PPW; ++k) {
             const int piece = wid * PPW + k;
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgradArgs a, i
                 const int iy = y0 - 1 + pr, ix = pc - 1;
                 uint32_t off = WH_OOB;
                 if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                    off = ((uint32_t)(img * a.H + iy) * a.W + (uint32_t)ix) * ldx + (uint32_t)(wh_slot(dslot, q) * 16);
+                    off = ((uint32_t)iy * a.W + (uint32_t)ix) * ldx + (uint32_t)(wh_slot(dslot, q) * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)lds, 16, off, 0,
                                                          0, 0);
             }
@@ -205,7 +208,7 @@ inline bool wgrad_halo_ok(const WgradArgs& a, bool wide = true, bool dflt = fals
     // 390 vs 364 us for the register-staged kernel at R50 512@7, batch 1024)
     const bool geo = (a.W == 56 && a.H % 4 == 0) || (a.W == 28 && a.H % 4 == 0) || (a.W == 14 && a.H % 14 == 0) ||
                      (a.W == 7 && a.H % 7 == 0 && !dflt);
-    return geo && (size_t)a.N * a.H * a.W * a.Ci * 2 < (1ull << 31) && (size_t)a.M * a.Co * 2 < (1ull << 31);
+    return geo && (size_t)a.H * a.W * a.Ci * 2 < (1ull << 31) && (size_t)a.OH * a.OW * a.Co * 2 < (1ull << 31);
 }
 
 template <int W, int R, int NKS, int PW>

@@ -67,22 +67,27 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
     const int dh = tap / a.KW - a.pad, dw = tap % a.KW - a.pad;
 
     // descriptors: the column offset (co0 / ci0) in the base, so a row's offset is row * ld * 2 +
-    // chunk * 16 and anything at or past row M (dY) is out of range
-    const __amdgpu_buffer_rsrc_t rd = wg3_rsrc(a.dY + co0, (uint32_t)((size_t)a.M * a.Co * 2 - co0 * 2));
-    const __amdgpu_buffer_rsrc_t rx =
-        wg3_rsrc(a.X + ci0, (uint32_t)((size_t)a.N * a.H * a.W * a.Ci * 2 - ci0 * 2));
+    // chunk * 16 and anything at or past row M (dY) is out of range. Both are based at the split's first row
+    // (dY) / first image (X, or first row when dense), so the 32-bit offsets hold for any tensor size
+    const int ohw = a.OH * a.OW;
+    const bool dense = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.OH == a.H && a.OW == a.W;
+    const size_t dro = (size_t)mbeg * a.Co;
+    const __amdgpu_buffer_rsrc_t rd =
+        wg3_rsrc(a.dY + dro + co0, (uint32_t)min(((size_t)a.M * a.Co - dro - co0) * 2, (size_t)0x7FFFFFFF));
+    const int img0 = mbeg / ohw;
+    const size_t xro = dense ? (size_t)mbeg * a.Ci : (size_t)img0 * a.H * a.W * a.Ci;
+    const __amdgpu_buffer_rsrc_t rx = wg3_rsrc(
+        a.X + xro + ci0, (uint32_t)min(((size_t)a.N * a.H * a.W * a.Ci - xro - ci0) * 2, (size_t)0x7FFFFFFF));
 
     // this lane's DMA slot: row (within the 4-row piece) and source chunk
     const int prow = lane >> 4;
-    const int ohw = a.OH * a.OW;
-    const bool dense = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.OH == a.H && a.OW == a.W;
     uint32_t voffd[PPW], rowcs[PPW];
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
         const int r = (wid * PPW + q) * 4 + prow;  // row within the stage
         const int ch = (lane & 15) ^ wg3_swz(r);
         rowcs[q] = (uint32_t)(ch * 16);
-        voffd[q] = (uint32_t)((mbeg + r) * a.Co * 2) + rowcs[q];
+        voffd[q] = (uint32_t)(r * a.Co * 2) + rowcs[q];
     }
     const uint32_t dstep = (uint32_t)(BR * a.Co * 2);
 
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
             const int m = mb + (wid * PPW + q) * 4 + prow;
             uint32_t off = WG3_OOB;
             if (dense) {
-                if (m < mend) off = (uint32_t)m * (uint32_t)(a.Ci * 2) + rowcs[q];
+                if (m < mend) off = (uint32_t)(m - mbeg) * (uint32_t)(a.Ci * 2) + rowcs[q];
             } else if (m < mend) {
                 const uint32_t img = fdiv((uint32_t)m, a.mg_ohw, a.sh_ohw);
                 const uint32_t rem = (uint32_t)m - img * (uint32_t)ohw;
@@ -108,8 +113,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
                 const uint32_t ow = rem - oh * (uint32_t)a.OW;
                 const int ih = (int)oh * a.stride + dh, iw = (int)ow * a.stride + dw;
                 if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                    off = ((img * (uint32_t)a.H + (uint32_t)ih) * (uint32_t)a.W + (uint32_t)iw) * (uint32_t)(a.Ci * 2) +
-                          rowcs[q];
+                    off = (((img - (uint32_t)img0) * (uint32_t)a.H + (uint32_t)ih) * (uint32_t)a.W + (uint32_t)iw) *
+                              (uint32_t)(a.Ci * 2) + rowcs[q];
             }
             wg3_dma(rx, dX + q * 1024, off);
         }
@@ -195,7 +200,9 @@ bool wgrad_v3_ok(const WgradArgs& a) {
     if (a.stem || a.xbn) return false;
     if (a.Co % 128 && !(a.Co == 64 && a.KH == 1 && a.KW == 1)) return false;  // (Co = 64: the same, on dY's rows)
     if (a.Ci % 128 && !(a.Ci == 64 && a.KH == 1 && a.KW == 1)) return false;
-    if ((size_t)a.M * a.Co * 2 >= (1u << 31) || (size_t)a.N * a.H * a.W * a.Ci * 2 >= (1u << 31)) return false;
+    // (descriptors based per split: one split's rows / images must stay below 2^31 bytes -- the launcher's
+    // splits keep a split to a few thousand rows; one image bound here)
+    if ((size_t)a.H * a.W * a.Ci * 2 * 8 >= (1u << 31) || (size_t)a.OH * a.OW * a.Co * 2 * 8 >= (1u << 31)) return false;
     return true;
 }
 
@@ -214,6 +221,10 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
     }
     int mps = (a.M + splits - 1) / splits;
     mps = (mps + BR - 1) / BR * BR;  // whole stages: a split's last stage never reads the next split's rows
+    // a split's dY rows / X images addressed by 32-bit offsets from its own base (kernel): keep each below 2^31
+    const size_t ohw = (size_t)a.OH * a.OW, img = (size_t)a.H * a.W * a.Ci * 2;
+    while (mps > BR && ((size_t)mps * a.Co * 2 >= (1u << 31) || ((size_t)mps / ohw + 2) * img >= (1u << 31)))
+        mps = (mps / 2 + BR - 1) / BR * BR;
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
     const size_t lds = (size_t)NS * 2 * BR * 256;

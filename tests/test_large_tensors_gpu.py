@@ -1,0 +1,85 @@
+"""Kernels on tensors past 2^31 bytes (a batch of 2048 images at 224 px puts 3.3 GB in one layer-1 activation).
+
+The GEMM-shaped kernels address their operands through 32-bit buffer offsets from a descriptor base; that base
+is per tile (v3 conv), per split (weight gradients), per band (halo kernels) or per pixel group (streaming 1x1),
+so any tensor size works. Each test runs a kernel on cat([x, x]) (> 2 GB) and checks the two halves against each
+other and against the same kernel on x alone: per-pixel results (forward, dgrad) bit for bit, the weight gradient
+as 2 x the half's up to summation order. (A whole-network comparison cannot do this: a random-init ResNet-50's
+gradient differs by O(1) between two runs of the SAME step, through the float-atomic summation order.)"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+GB2 = 2 ** 31
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def _pair(n, h, c, seed):
+    torch.manual_seed(seed)
+    x = torch.randn(n, h, h, c, device=DEV).to(torch.bfloat16)
+    x2 = torch.cat([x, x])
+    assert x2.numel() * 2 > GB2
+    return x, x2
+
+
+def _halves_equal(y2, y):
+    n = y.shape[0]
+    assert torch.equal(y2[:n], y2[n:]), "the two halves differ"
+    assert torch.equal(y2[:n], y), "the large launch differs from the small one"
+
+
+@pytest.mark.parametrize("tile", [17, 18])
+def test_v3_conv_past_2gb(tile):
+    """v3 main loop (explicit tiles: 256x256 / 128x128), 3x3 256 -> 256 @14 forward and dgrad."""
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
+    x, x2 = _pair(22000, 14, 256, 1)
+    w = (torch.randn(256, 3, 3, 256, device=DEV) * 0.02).to(torch.bfloat16)
+    _halves_equal(igemm_fwd(x2, w, 1, 1, 3, 3, tile=tile), igemm_fwd(x, w, 1, 1, 3, 3, tile=tile))
+    wt = w.permute(3, 1, 2, 0).contiguous()  # [Ci][KH][KW][Co]
+    _halves_equal(igemm_dgrad(x2, wt, (14, 14), 1, 1, 3, 3, tile=tile), igemm_dgrad(x, wt, (14, 14), 1, 1, 3, 3, tile=tile))
+
+
+def test_stream_conv_past_2gb():
+    """streaming 1x1 kernel (K = 256 -> 64 and 64 -> 256 @56, batch 2 x 1100)."""
+    from imagent_amd.ops.conv import igemm_fwd
+    x, x2 = _pair(1100, 56, 256, 2)
+    w = (torch.randn(64, 1, 1, 256, device=DEV) * 0.05).to(torch.bfloat16)
+    _halves_equal(igemm_fwd(x2, w, 1, 0, 1, 1), igemm_fwd(x, w, 1, 0, 1, 1))
+    h, h2 = x[..., :64].contiguous(), x2[..., :64].contiguous()
+    w3 = (torch.randn(256, 1, 1, 64, device=DEV) * 0.1).to(torch.bfloat16)
+    _halves_equal(igemm_fwd(h2, w3, 1, 0, 1, 1), igemm_fwd(h, w3, 1, 0, 1, 1))
+
+
+def test_halo_conv_past_2gb():
+    """halo-tiled 64 -> 64 3x3 @56 forward and dgrad."""
+    from imagent_amd.ops.conv import igemm_dgrad, igemm_fwd
+    x, x2 = _pair(5600, 56, 64, 3)
+    w = (torch.randn(64, 3, 3, 64, device=DEV) * 0.05).to(torch.bfloat16)
+    _halves_equal(igemm_fwd(x2, w, 1, 1, 3, 3), igemm_fwd(x, w, 1, 1, 3, 3))
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    _halves_equal(igemm_dgrad(x2, wt, (56, 56), 1, 1, 3, 3), igemm_dgrad(x, wt, (56, 56), 1, 1, 3, 3))
+
+
+@pytest.mark.parametrize("variant,shape", [(1, (22000, 14, 256, 256, 1)), (0, (5600, 56, 64, 64, 3)),
+                                           (-1, (1100, 56, 256, 64, 1))],
+                         ids=["wgrad_v3_1x1", "wgrad_halo_3x3", "wgrad_regstaged_1x1"])
+def test_wgrad_past_2gb(variant, shape):
+    """weight gradients (LDS-DMA v3 / halo-tiled / register-staged) over > 2 GB operands: dW(cat) = 2 dW(half)."""
+    from imagent_amd.ops.conv import igemm_wgrad
+    n, h, ci, co, k = shape
+    x, x2 = _pair(n, h, ci, 4)
+    torch.manual_seed(5)
+    g = torch.randn(n, h, h, co, device=DEV).to(torch.bfloat16)
+    g2 = torch.cat([g, g])
+    dw = torch.zeros(co, k * k * ci, device=DEV)
+    dw2 = torch.zeros_like(dw)
+    igemm_wgrad(g, x, dw, 1, k // 2, k, k, variant=variant)
+    igemm_wgrad(g2, x2, dw2, 1, k // 2, k, k, variant=variant)
+    assert rel(dw2, 2 * dw) < 1e-3

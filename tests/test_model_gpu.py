@@ -511,3 +511,4 @@ def test_eval_forward_224_matches_torch(arch):
     e = rel(got, r32)
     print(f"{arch} eval logits: hip {e:.4f} autocast-bf16 {ebf:.4f}")
     assert e < max(5e-2, 2.0 * ebf), (e, ebf)
+
