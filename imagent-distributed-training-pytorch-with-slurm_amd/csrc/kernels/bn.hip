@@ -115,18 +115,96 @@ __device__ __forceinline__ void stq(bf16_t* p, const float (&o)[8], uint32_t* q,
 }
 
 
+// ---------------------------------------------------------------- slab fold inside the consumer
+// The fold of a producer's [S][Q][C] statistics slab (formerly its own launch before every BN pass: stats_finalize_mv
+// forward, stats_finalize backward) done by the consumer pass itself: the first ceil(n / 256) blocks each fold 256 of
+// the n quantities, store them, and publish with an agent-scope release + counter (cdna_hip_programming.md
+// Guideline 16 R1: sc1 stores, vmcnt(0) per wave, barrier, relaxed agent fetch_add); every block
+// workgroup waits for the counter (one lane's relaxed polls, one acquire fence, a barrier) before using them. The folding blocks are the lowest block ids, dispatched first, and never wait on a later
+// block: no deadlock whatever the residency. The counter (zero at launch: zeroed with the slabs once per step) lives
+// in the BN's backward scratch (imk_bn_bwd_scratch_floats' last row).
+constexpr int FOLD_S = 32;  // slab slots the in-pass fold supports (STAT_SLOTS = BWD_SLOTS = 32; host-checked)
+static_assert(BWD_SLOTS == FOLD_S, "backward slab slots");
+struct SlabFold {
+    const float* slab;   // [S][n] (backward) or [S][2][C] shifted sums (forward); null: no fold, `out` is ready
+    const float* shift;  // forward: the shift the sums were taken around (the previous batch mean) or null
+    float* out;          // backward: [n] sums; forward: [2][C] (mean, biased variance)
+    uint32_t* cnt;       // publish counter, zero at launch (zeroed with the slabs once per step)
+    int S;
+    float inv_cnt;       // forward only
+};
+
+__device__ __forceinline__ void fold_publish(const SlabFold& f, int n, bool fwd, int C) {
+    const int nfold = (n + 255) / 256;
+    if ((int)blockIdx.x < nfold) {
+        const int i = blockIdx.x * 256 + threadIdx.x;
+        if (i < n) {
+            // all FOLD_S slot loads issued before the adds (one L2 round trip, not S dependent ones: the rest of the
+            // grid waits on this), summed in the separate launches' order
+            if (fwd) {  // channel i: mean = shift + E[d], var = E[d^2] - E[d]^2 (fixed order, as stats_finalize_mv)
+                float va[FOLD_S], vb[FOLD_S];
+#pragma unroll
+                for (int k = 0; k < FOLD_S; ++k) {
+                    va[k] = f.slab[(size_t)k * 2 * C + i];
+                    vb[k] = f.slab[(size_t)k * 2 * C + C + i];
+                }
+                float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < FOLD_S; ++k) {
+                    a[k & 3] += va[k];
+                    b[k & 3] += vb[k];
+                }
+                const float m1 = ((a[0] + a[1]) + (a[2] + a[3])) * f.inv_cnt;
+                const float m2 = ((b[0] + b[1]) + (b[2] + b[3])) * f.inv_cnt;
+                __hip_atomic_store(f.out + i, (f.shift ? f.shift[i] : 0.f) + m1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1): no release fence needed
+                __hip_atomic_store(f.out + C + i, fmaxf(m2 - m1 * m1, 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {  // quantity i: plain sum over the slots (as stats_finalize_kernel)
+                float v[FOLD_S];
+#pragma unroll
+                for (int k = 0; k < FOLD_S; ++k) v[k] = f.slab[(size_t)k * n + i];
+                float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < FOLD_S; ++k) a[k & 3] += v[k];
+                __hip_atomic_store(f.out + i, (a[0] + a[1]) + (a[2] + a[3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// per workgroup (every thread of the block must call it): ONE lane polls the counter (relaxed, long sleeps: the
+// grid's pollers share one word), the barrier releases the block; the payload was stored sc1 and is read sc1 (no
+// L1 invalidate: Guideline 16, R1 with sc1 consumer loads)
+__device__ __forceinline__ void fold_wait(const SlabFold& f, int n) {
+    const uint32_t nfold = (uint32_t)((n + 255) / 256);
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(f.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nfold)
+            __builtin_amdgcn_s_sleep(32);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: every later load of the
+    __syncthreads();                                         //  folded values is an sc1 load, fld())
+}
+
+// a folded value: sc1 (agent-scope relaxed) load when it was published inside this launch, else a plain load
+__device__ __forceinline__ float fld(const float* p, bool sc) {
+    return sc ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+
 // ---------------------------------------------------------------- forward
 // y = relu?( (x-mean)*rstd*g + b  [+ res | + (x2-mean2)*rstd2*g2 + b2] )
 // NT: non-temporal output stores; Q8: also the e4m3 copy y8 (fp8 path; the plain kernel carries none
 // of its code: 94 -> fewer VGPRs)
 template <int MODE, bool RELU, bool NT, bool Q8>  // MODE 0: none, 1: identity residual, 2: second BN branch
 __global__ __launch_bounds__(256) void bn_fwd_kernel(
-    const bf16_t* __restrict__ x, const float* __restrict__ sums, const float* __restrict__ gamma,
+    const bf16_t* __restrict__ x, const float* sums, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ x2, const float* __restrict__ sums2,
     const float* __restrict__ gamma2, const float* __restrict__ beta2, bf16_t* __restrict__ y,
     float* __restrict__ save, float* __restrict__ save2, long R, int C, float inv_cnt, float eps,
     int eval, uint32_t* __restrict__ y8, const int* __restrict__ exp8, float* __restrict__ amax8,
-    uint8_t* __restrict__ ym, float* __restrict__ colsum) {
+    uint8_t* __restrict__ ym, float* __restrict__ colsum, SlabFold fold) {
+    if (fold.slab) fold_publish(fold, C, true, C);  // (mode 0; `sums` is fold.out: read after fold_wait)
     const int cpr = C / 8;                // chunks per row
     const int rpb = 256 / cpr;            // rows per block-iteration (C <= 2048)
     const int tid = threadIdx.x;
@@ -139,14 +217,23 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(
     float cs[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cs[i] = 0.f;
+    if (fold.slab) fold_wait(fold, C);
     if (tid >= rpb * cpr) return;  // (host: with y8, every lane is active -- C/8 divides 256)
     const int ch = tid % cpr, c0 = ch * 8;
     float sc[8], sh[8], sc2[8], sh2[8];
     // per-channel constants by 16-B loads (c0 % 8 == 0, 32-B aligned arrays)
     auto consts = [&](const float* su, const float* g, const float* b, float* sv, float (&k)[8], float (&o)[8]) {
         float s0[8], s1[8], gg[8], bb[8];
-        ld8f(su + c0, s0);
-        ld8f(su + C + c0, s1);
+        if (fold.slab && su == sums) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                s0[i] = fld(su + c0 + i, true);
+                s1[i] = fld(su + C + c0 + i, true);
+            }
+        } else {
+            ld8f(su + c0, s0);
+            ld8f(su + C + c0, s1);
+        }
         ld8f(g + c0, gg);
         ld8f(b + c0, bb);
 #pragma unroll
@@ -541,10 +628,15 @@ template <int MASK, int MODE, bool NT, bool Q8>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
-    const float* __restrict__ scratch, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+    const float* scratch, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
     const bf16_t* __restrict__ x2, const float* __restrict__ save2, const float* __restrict__ gamma2,
     bf16_t* __restrict__ dx2, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8, int sgxo) {
+    float* __restrict__ dgamma2, float* __restrict__ dbeta2, long R, int C, float inv_cnt, G8Out g8, int sgxo,
+    SlabFold fold) {
+    if (fold.slab) {  // (`scratch` is fold.out)
+        fold_publish(fold, 3 * C, false, C);
+        fold_wait(fold, 3 * C);
+    }
     constexpr int UB = MODE == 2 ? 2 : U;  // three streams in, two out: half the rows in flight
     const int cpr = C / 8, rpb = 256 / cpr, tid = threadIdx.x;
     const float qs0 = Q8 && g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
@@ -552,11 +644,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     float m0 = 0.f, m1 = 0.f;
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
-            if (dgamma) dgamma[c] += scratch[sgxo + c];
-            if (dbeta) dbeta[c] += scratch[C + c];
+            const bool sc = fold.slab != nullptr;
+            if (dgamma) dgamma[c] += fld(scratch + sgxo + c, sc);
+            if (dbeta) dbeta[c] += fld(scratch + C + c, sc);
             if (MODE == 2) {
-                if (dgamma2) dgamma2[c] += scratch[2 * C + c];
-                if (dbeta2) dbeta2[c] += scratch[C + c];
+                if (dgamma2) dgamma2[c] += fld(scratch + 2 * C + c, sc);
+                if (dbeta2) dbeta2[c] += fld(scratch + C + c, sc);
             }
         }
     }
@@ -572,15 +665,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             sc[i] = gr;
             sh[i] = beta[c] - mean * gr;
         }
+        const bool sc = fold.slab != nullptr;
         k1[i] = gr;
-        kx[i] = -gr * inv_cnt * scratch[sgxo + c] * rstd;
-        k0[i] = -gr * inv_cnt * scratch[C + c] - kx[i] * mean;
+        kx[i] = -gr * inv_cnt * fld(scratch + sgxo + c, sc) * rstd;
+        k0[i] = -gr * inv_cnt * fld(scratch + C + c, sc) - kx[i] * mean;
         if (MODE == 2) {
             const float m2 = save2[c], rs2 = save2[C + c];
             const float g2 = gamma2[c] * rs2;
             q1[i] = g2;
-            qx[i] = -g2 * inv_cnt * scratch[2 * C + c] * rs2;
-            q0[i] = -g2 * inv_cnt * scratch[C + c] - qx[i] * m2;
+            qx[i] = -g2 * inv_cnt * fld(scratch + 2 * C + c, sc) * rs2;
+            q0[i] = -g2 * inv_cnt * fld(scratch + C + c, sc) - qx[i] * m2;
         }
     }
     const long step = rpb;  // block-contiguous rows (see bn_fwd_kernel)
@@ -684,19 +778,23 @@ IMK_EXPORT int imk_bn_fwd(const void* x, const float* sums, const float* gamma, 
                           const void* x2, const float* sums2, const float* gamma2, const float* beta2,
                           void* y, float* save, float* save2, long R, int C, int mode, int relu,
                           float eps, int eval, void* y8, const int* exp8, float* amax8, void* ym,
-                          float* colsum, void* stream) {
+                          float* colsum, const float* fslab, const float* fshift, void* fcnt, int fS,
+                          void* stream) {
     if (C % 8 || C > 2048) return -100;
     if (y8 && (256 % (C / 8) || !exp8 || !amax8)) return -102;
     if (colsum && (mode != 0 || 256 % (C / 8))) return -103;
+    // fslab: fold the conv epilogue's [fS][2][C] shifted-sum slab into `sums` inside this pass (mode 0, training)
+    if (fslab && (mode != 0 || eval || !fcnt || fS != FOLD_S)) return -104;
+    const SlabFold fold{fslab, fshift, const_cast<float*>(sums), static_cast<uint32_t*>(fcnt), fS, 1.f / (float)R};
     const float inv_cnt = 1.f / (float)R;
-    const int grid = grid_for(R, C);
+    const int grid = std::max(grid_for(R, C), fslab ? (C + 255) / 256 : 1);
     hipStream_t st = (hipStream_t)stream;
     const bool nt = bn_nt(), q8 = y8 != nullptr;
 #define LK(M, RL, NT, Q8)                                                                               \
     hipLaunchKernelGGL((bn_fwd_kernel<M, RL, NT, Q8>),                                                  \
                        dim3(resident_grid((const void*)bn_fwd_kernel<M, RL, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)x, sums, \
                        gamma, beta, (const bf16_t*)x2, sums2, gamma2, beta2, (bf16_t*)y, save, save2, R, C,   \
-                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym, colsum)
+                       inv_cnt, eps, eval, (uint32_t*)y8, exp8, amax8, (uint8_t*)ym, colsum, fold)
 #define L(M, RL)                                              \
     do {                                                      \
         if (q8) { if (nt) LK(M, RL, true, true); else LK(M, RL, false, true); }   \
@@ -737,7 +835,7 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
                                 const void* x2, const float* save2, const float* gamma2, float* scratch,
                                 void* dx, void* dx2, float* dgamma_acc, float* dbeta_acc, float* dgamma2_acc,
                                 float* dbeta2_acc, long R, int C, int mode, const void* g8desc, int sgx_row,
-                                void* stream) {
+                                int fold_in, void* stream) {
     // sgx_row (mode 0 / 1): the slab row holding sum(g xhat) -- 2 when `scratch` is a Gram-form bn3's slab whose
     // third row the producing dgrad filled with the downsample BN's sum(g xhat_d) (ops/block.py)
     if (C % 8 || C > 2048 || sgx_row < 0 || sgx_row > 2 || (mode == 2 && sgx_row)) return -100;
@@ -756,10 +854,17 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     }
     hipStream_t st = (hipStream_t)stream;
     float* folded = scratch + (size_t)BWD_SLOTS * 3 * C;
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
-                       BWD_SLOTS, 3 * C);
-    IMK_CHECK_LAUNCH();
-    const int grid = grid_for(R, C);
+    // fold_in: the apply pass folds the slab itself (SlabFold; its counter in the scratch's last row), else one
+    // launch of its own
+    SlabFold fold{};
+    if (fold_in) {
+        fold = SlabFold{scratch, nullptr, folded, reinterpret_cast<uint32_t*>(folded + 3 * C), BWD_SLOTS, 0.f};
+    } else {
+        hipLaunchKernelGGL(stats_finalize_kernel, dim3((3 * C + 63) / 64), dim3(64), 0, st, scratch, folded,
+                           BWD_SLOTS, 3 * C);
+        IMK_CHECK_LAUNCH();
+    }
+    const int grid = std::max(grid_for(R, C), fold_in ? (3 * C + 255) / 256 : 1);
     const float inv_cnt = 1.f / (float)R;
     const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1];
 #define LK(M, NT, Q8)                                                                                \
@@ -767,7 +872,7 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
                        dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
                        nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr,       \
                        (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,               \
-                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8, sgx_row * C)
+                       dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8, sgx_row * C, fold)
 #define LA(M)                                                                  \
     do {                                                                       \
         if (q8) { if (nt) LK(M, true, true); else LK(M, false, true); }        \
@@ -780,7 +885,8 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     return 0;
 }
 
-IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 3) * C; }
+// [BWD_SLOTS][3][C] slab, folded [3][C], one more row: word 0 the backward fold's counter, word 1 the forward's
+IMK_EXPORT int imk_bn_bwd_scratch_floats(int C) { return (BWD_SLOTS * 3 + 4) * C; }
 
 // forward statistics: shifted-sum slab [S][2][C] -> out [2][C] = (mean, biased variance)
 // deterministic mode on / off; on: allocates the partial-row workspace once (no allocation inside a capture)
@@ -865,7 +971,7 @@ IMK_EXPORT int imk_bn_bwd(const void* dy, const void* y, const void* x, const fl
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, M, false, false>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, \
                        (const bf16_t*)y, (const bf16_t*)x, save, gamma, beta, folded, (bf16_t*)dx,   \
                        (bf16_t*)dres, (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc,    \
-                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{}, 0)
+                       dbeta_acc, dgamma2_acc, dbeta2_acc, R, C, inv_cnt, G8Out{}, 0, SlabFold{})
     if (mode == 0) { if (relu == 2) LA(2, 0); else if (relu) LA(1, 0); else LA(0, 0); }
     else if (mode == 1) { if (relu) LA(1, 1); else LA(0, 1); }
     else { if (relu) LA(1, 2); else LA(0, 2); }

@@ -164,9 +164,9 @@ def _declare(name: str, lib) -> None:
             "imk_normalize_u8_f32": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_xent_bwd_f32": [vp, vp, vp, vp, vp, i32, i32, f32, vp],
             "imk_bn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, f32, i32, vp, vp, vp,
-                           vp, vp, vp],
+                           vp, vp, vp, vp, vp, i32, vp],
             "imk_bn_bwd": [vp] * 17 + [i64, i32, i32, i32, vp],
-            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, i32, vp],
+            "imk_bn_bwd_apply": [vp] * 14 + [i64, i32, i32, vp, i32, i32, vp],
             "imk_bn_running_update": [vp, i32, vp],
             "imk_bn_eval_affine": [vp, i32, vp],
             "imk_set_deterministic": [i32],

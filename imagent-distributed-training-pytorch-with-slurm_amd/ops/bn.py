@@ -54,18 +54,29 @@ def bn_scale_shift(x: torch.Tensor, bn) -> torch.Tensor:
 
 
 def bn_fwd_launch(x, stats, gamma, beta, y, save, *, x2=None, stats2=None, gamma2=None, beta2=None,
-                  save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False, q8=None, ym=None, colsum=None):
+                  save2=None, mode=0, relu=True, eps=1e-5, eval_mode=False, q8=None, ym=None, colsum=None,
+                  fold=None):
     """``q8 = (y8 uint8, exp int32[1], amax f32[1])``: also write the e4m3 copy of y.
     ``ym`` (uint8, numel / 8; modes 1 / 2 with ReLU): also write the mask y > 0 as bits.
-    ``colsum`` (fp32 [C], zeroed; mode 0): also accumulate the column sums of the stored y."""
+    ``colsum`` (fp32 [C], zeroed; mode 0): also accumulate the column sums of the stored y.
+    ``fold`` (mode 0, training): the BN's ``work``: the pass folds ``work.slab`` into ``stats`` itself (the
+    former :func:`stats_finalize` launch; its counter in ``work.scratch``'s last row)."""
     C = x.shape[-1]
     R = x.numel() // C
     y8, e8, a8 = q8 if q8 is not None else (None, None, None)
+    fslab = fshift = fcnt = None
+    fS = 0
+    if fold is not None:
+        from .conv import _SHIFT
+        fslab, fS = fold.slab.data_ptr(), fold.slab.shape[0]
+        fshift = fold.save.data_ptr() if _SHIFT else None
+        fcnt = fold.scratch.data_ptr() + 4 * (fold.scratch.numel() - C + 1)  # word 1 of the last row
     _lib.check(_lib.kernels().imk_bn_fwd(
         x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), _lib.ptr(x2),
         _lib.ptr(stats2), _lib.ptr(gamma2), _lib.ptr(beta2), y.data_ptr(), _lib.ptr(save),
         _lib.ptr(save2), R, C, mode, 1 if relu else 0, eps, 1 if eval_mode else 0,
-        _lib.ptr(y8), _lib.ptr(e8), _lib.ptr(a8), _lib.ptr(ym), _lib.ptr(colsum), _lib.stream_ptr()), "bn fwd")
+        _lib.ptr(y8), _lib.ptr(e8), _lib.ptr(a8), _lib.ptr(ym), _lib.ptr(colsum), fslab, fshift, fcnt, fS,
+        _lib.stream_ptr()), "bn fwd")
 
 
 def relu_mask_bits(y: torch.Tensor) -> torch.Tensor:
@@ -83,10 +94,12 @@ def bn_act_forward(x: torch.Tensor, x2: Optional[torch.Tensor], bn, bn2, mode: i
     y = torch.empty_like(x)
     w, w2 = bn.work, (bn2.work if bn2 is not None else None)
     R = x.numel() // x.shape[-1]
-    stats_finalize(w, R)
+    fold = w if (mode == 0 and w.scratch is not None) else None  # mode 0: the apply pass folds its own slab
+    if fold is None:
+        stats_finalize(w, R)
     if w2 is not None:
         stats_finalize(w2, R)
-    bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2,
+    bn_fwd_launch(x, w.stats, bn.weight, bn.bias, y, w.save, x2=x2, fold=fold,
                   stats2=w2.stats if w2 is not None else None,
                   gamma2=bn2.weight if bn2 is not None else None,
                   beta2=bn2.bias if bn2 is not None else None,
@@ -129,7 +142,7 @@ def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tenso
                       mode: int, g8=None, slab_of=None, sgx_row: int = 0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Backward of act(bn(x) [+ res | + bn2(x2)]) for a gradient ``g`` that its
     producing dgrad already ReLU-masked and reduced into ``bn.work.scratch``
-    (``ops.conv.BNBwdFuse``): one fold + one streaming apply pass.
+    (``ops.conv.BNBwdFuse``): one streaming apply pass that folds the slab itself (``SlabFold``, bn.hip).
     Returns (dx, dx2 | None); for mode 1 the residual-branch gradient is g.
     ``g8 = ((q, exp, amax) | None, (q2, exp2, amax2) | None)``: also write e5m2
     copies of dx / dx2 for the fp8 dgrad (``Fp8State``).
@@ -146,7 +159,7 @@ def bn_apply_backward(g: torch.Tensor, x: torch.Tensor, x2: Optional[torch.Tenso
         bn2.work.save.data_ptr() if mode == 2 else 0, bn2.weight.data_ptr() if mode == 2 else 0,
         scratch.data_ptr(), dx.data_ptr(), _lib.ptr(dx2), bn.weight.grad.data_ptr(),
         bn.bias.grad.data_ptr(), bn2.weight.grad.data_ptr() if mode == 2 else 0,
-        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _g8desc(g8), sgx_row, _lib.stream_ptr()),
+        bn2.bias.grad.data_ptr() if mode == 2 else 0, R, C, mode, _g8desc(g8), sgx_row, 1, _lib.stream_ptr()),
         "bn bwd apply")
     notify_ready(bn.weight)
     notify_ready(bn.bias)

@@ -206,3 +206,51 @@ def test_gram_statistics_large_mean(p):
     e_sgx = float(((bn.weight.grad.double() - ref).abs() / ref.abs()).max())
     print(f"p={p}: x-free sum(g xhat) rel err {e_sgx:.2e}")
     assert float(ref.abs().min()) > 0.1 * M and e_sgx < 1e-3
+
+
+@pytest.mark.parametrize("C,R", [(64, 5000), (512, 3000), (2048, 700)])
+def test_slab_fold_inside_the_pass(C, R):
+    """The BN passes fold their statistics slab themselves (SlabFold, bn.hip: the first blocks fold and publish,
+    every wave waits on the counter): forward statistics / output and the backward's folded sums and dx equal the
+    former separate fold launch's bit for bit."""
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.bn import bn_fwd_launch, stats_finalize
+    torch.manual_seed(7)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    x = torch.randn(R, C, device=DEV).to(torch.bfloat16)
+    a, b = _work(C), _work(C)
+    for rep in range(3):
+        a.slab.copy_(torch.randn_like(a.slab) * (rep + 1))
+        a.save.copy_(torch.randn_like(a.save))
+        b.slab.copy_(a.slab)
+        b.scratch.zero_()  # the fold's publish counter (zeroed with the slabs once per step in the model)
+        save0 = a.save.clone()
+        ya, yb = torch.empty_like(x), torch.empty_like(x)
+        b.save.copy_(save0)
+        stats_finalize(a, R)
+        bn_fwd_launch(x, a.stats, gamma, beta, ya, a.save)
+        bn_fwd_launch(x, b.stats, gamma, beta, yb, b.save, fold=b)
+        torch.cuda.synchronize()
+        assert torch.equal(a.stats, b.stats), rep
+        assert torch.equal(ya, yb) and torch.equal(a.save, b.save), rep
+    # backward: apply with the fold inside vs the separate launch, on identical slabs
+    g = torch.randn(R, C, device=DEV).to(torch.bfloat16)
+    k = _lib.kernels()
+    res = []
+    for fold_in in (0, 1, 1):
+        w = _work(C)
+        torch.manual_seed(8)
+        nb = 32 * 3 * C
+        w.scratch[:nb].copy_(torch.randn(nb, device=DEV))
+        w.save.copy_(torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5]))
+        dx = torch.empty_like(x)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        _lib.check(k.imk_bn_bwd_apply(g.data_ptr(), x.data_ptr(), w.save.data_ptr(), gamma.data_ptr(), None, None,
+                                      None, w.scratch.data_ptr(), dx.data_ptr(), None, dg.data_ptr(), db.data_ptr(),
+                                      None, None, R, C, 0, None, 0, fold_in, _lib.stream_ptr()), "apply")
+        torch.cuda.synchronize()
+        res.append((dx, w.scratch[nb:nb + 3 * C].clone(), dg, db))
+    for r in res[1:]:
+        assert torch.equal(r[0], res[0][0]) and torch.equal(r[1], res[0][1])
+        assert torch.equal(r[2], res[0][2]) and torch.equal(r[3], res[0][3])
