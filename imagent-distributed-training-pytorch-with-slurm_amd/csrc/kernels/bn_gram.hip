@@ -142,18 +142,27 @@ __global__ __launch_bounds__(256) void bn_gram_gemm_kernel(const bf16_t* __restr
 // dW3 [C4][p] += A_o T[o][i] + B_o P[o][i] + (c_o + B_o mean_o) s[i]   (T = g^T h2, P = W3 Gc with the centred
 // Gram matrix, s = colsum h2). From dW3 = dx3^T h2 = A T + B W3 G + c s^T and W3 G = P + mean s^T: the centred form
 // adds no two large, nearly equal terms when |mean| >> std (c_o + B_o mean_o = -A_o mean(g) is small)
-__global__ __launch_bounds__(256) void bn_gram_wgrad_fixup_kernel(float* __restrict__ dw,
+__global__ __launch_bounds__(64) void bn_gram_wgrad_fixup_kernel(float* __restrict__ dw,
                                                                   const float* __restrict__ T,
                                                                   const float* __restrict__ P,
                                                                   const float* __restrict__ coef,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ s, int C4, int p) {
-    const long n = (long)C4 * p;
-    for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-        const int o = (int)(e / p), i = (int)(e - (long)o * p);
-        const float k0 = fmaf(coef[C4 + o], mean[o], coef[2 * C4 + o]);
-        dw[e] += fmaf(coef[o], T[e], fmaf(coef[C4 + o], P[e], k0 * s[i]));
-    }
+    // one wave per (row o, 256 columns): the row's three coefficients are wave-uniform scalar loads, 4 columns per
+    // lane; p is a multiple of 4 (the host checks), so every row starts 16-B aligned
+    const int o = blockIdx.y;
+    const int i = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (i >= p) return;
+    const float a = coef[o], b = coef[C4 + o], k0 = fmaf(b, mean[o], coef[2 * C4 + o]);
+    const long e = (long)o * p + i;
+    const float4 t = *reinterpret_cast<const float4*>(T + e), q = *reinterpret_cast<const float4*>(P + e);
+    const float4 sv = *reinterpret_cast<const float4*>(s + i);
+    float4 d = *reinterpret_cast<const float4*>(dw + e);
+    d.x += fmaf(a, t.x, fmaf(b, q.x, k0 * sv.x));
+    d.y += fmaf(a, t.y, fmaf(b, q.y, k0 * sv.y));
+    d.z += fmaf(a, t.z, fmaf(b, q.z, k0 * sv.z));
+    d.w += fmaf(a, t.w, fmaf(b, q.w, k0 * sv.w));
+    *reinterpret_cast<float4*>(dw + e) = d;
 }
 
 // As bn_bwd_coef_kernel, with sum(g xhat) NOT from the slab but from T = g^T h2 (the weight gradient's GEMM):
@@ -283,10 +292,8 @@ IMK_EXPORT int imk_bn_gram_p(const void* w, const float* G, const float* s, floa
 
 IMK_EXPORT int imk_bn_gram_wgrad_fixup(float* dw, const float* T, const float* P, const float* coef,
                                        const float* mean, const float* s, int C4, int p, void* stream) {
-    if (p <= 0 || C4 <= 0) return -100;
-    const long n = (long)C4 * p;
-    const int grid = (int)std::min<long>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(bn_gram_wgrad_fixup_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dw, T, P, coef,
+    if (p <= 0 || C4 <= 0 || C4 > 65535 || p % 4) return -100;
+    hipLaunchKernelGGL(bn_gram_wgrad_fixup_kernel, dim3((p + 255) / 256, C4), dim3(64), 0, (hipStream_t)stream, dw, T, P, coef,
                        mean, s, C4, p);
     IMK_CHECK_LAUNCH();
     return 0;
