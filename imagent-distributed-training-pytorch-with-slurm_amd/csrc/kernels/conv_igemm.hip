@@ -8,7 +8,7 @@
 //  * 64 -> 64 3x3 stride 1: the halo-tiled kernel (conv_halo.hip);
 //  * 1x1 with C in {64, 128, 256, 512}: the streaming kernel (conv_stream.hip);
 //  * C % 64 == 0 with the staged epilogue (every long-K conv, every fused BN-backward dgrad):
-//    the v3 main loop (conv_igemm_v3.h), 256x256 tiles for Nout >= 512, else 128x128
+//    the v3 main loop (conv_igemm_v3.h), 256x256 tiles for Nout >= 256 (enough tiles), else 128x128
 //    (round-3 A/B at R50 / 1024 img, profiles/r50_b1024_conv_v3.md);
 //  * the rest (C % 64 != 0, direct epilogues, Nout <= 64): the LDS-DMA ring / register-staged
 //    kernels of conv_igemm_impl.h.
@@ -23,6 +23,10 @@
 // per CU) overlaps one block's epilogue with the other's main loop, which is what the epilogue-heavy short-K
 // BN-backward dgrads need (A/B at batch 1024: 12,782 img/s with every conv on the big tile, 12,872 at 512)
 constexpr int V3_BIG_MIN_K = 512;
+// Narrowest output that takes the 256x256 v3 tile: 256 channels (one tile spans the whole output, so every pixel
+// row is fetched once; in-step A/B at 2048 img: 16,597 / 16,586 vs 16,469 / 16,488 img/s with 512; isolated
+// 256 -> 1024 @14 dgrad 327 vs 365 us, 512 -> 256 @28 fwd 842 vs 895 us)
+constexpr int V3_BIG_MIN_N = 256;
 
 // Wave-quantisation tail of the one-tile-per-block 256x256 kernels (one block per CU): with T tiles on S CUs the
 // last of ceil(T / S) rounds runs T mod S tiles on an otherwise idle chip (R50 at 1024 img: 784 tiles on 256 CUs =
@@ -108,7 +112,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         }
         if (!v3_ok(a) || a.Nout % 64) return -106;
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
-        if (a.Nout >= 512 && t8 >= 192) return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+        if (a.Nout >= V3_BIG_MIN_N && t8 >= 192) return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
         if (a.Nout == 64) return launch_v3<128, 64, 1, 2, 4, 128>(a, st);
         return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
@@ -168,7 +172,7 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
         // (the fused BN-backward dgrads on 128x128 tiles with their epilogue operands prefetched instead: within
         // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken)
-        if (a.Nout >= 512 && t8 >= 192 && K >= V3_BIG_MIN_K) {
+        if (a.Nout >= V3_BIG_MIN_N && t8 >= 192 && K >= V3_BIG_MIN_K) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles
                 IGemmArgs m = a, t = a;
