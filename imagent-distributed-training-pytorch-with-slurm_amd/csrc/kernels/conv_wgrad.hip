@@ -361,6 +361,12 @@ IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int var
         case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
         case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
         case 4: return launch_wgrad_v3<128, 2>(a, splits, st);
+        // 256 x 256 tile on 16 waves, one block per CU (64-row stages x 2): isolated 1x1 wgrads at 2048 img 12-26 %
+        // faster on the strided / 28x28 / 1024 -> 512 shapes, 2-4 % on the rest (32-row x 4 stages and the 8-wave
+        // 128 x 256 / 256 x 128 tiles measured slower than the 128 x 128 tile); in-step neutral as the 1x1 default
+        // (16,527 / 16,572 vs 16,522 / 16,542 img/s: its 128-KB blocks do not co-reside with the main stream's), so
+        // not dispatched (scripts/wgrad_ab.py --set 1x1, README round 5)
+        case 6: return wgrad_v3w_ok<4, 4>(a) ? launch_wgrad_v3<64, 2, 4, 4>(a, splits, st) : -106;
         default: return -106;
     }
 }

@@ -39,26 +39,35 @@ __device__ __forceinline__ void wg3_dma(__amdgpu_buffer_rsrc_t r, char* lds, uin
 
 __device__ __forceinline__ int wg3_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-// BR: pixel rows per stage (multiple of 32); NS: ring depth. 4 waves, 2 x 2 over a 128 x 128 tile.
-template <int BR, int NS>
-__global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
-    constexpr int SB = BR * 256;          // bytes per operand per stage
-    constexpr int PPW = BR / 16;          // 1-KB pieces per wave per operand per stage
-    constexpr int LPS = 2 * PPW;          // DMA instructions per wave per stage
+// BR: pixel rows per stage (multiple of 32); NS: ring depth. WCO x WKC waves of 64 x 64 over a (64 WCO) x (64 WKC)
+// tile: 2 x 2 (128 x 128, two blocks per CU) or wider tiles of one block per CU (256 x 256: 16 waves), which fetch
+// half the operand bytes per MFMA FLOP -- the L2 -> LDS path, not the MFMA, bounds the 128 x 128 tile. A tile
+// wider than 128 channels is staged as 128-channel sub-images of the same 256-B-row layout (sub-image h: channels
+// 128 h .. 128 h + 127 of every row of the stage), so the DMA pieces and the transposed reads are unchanged.
+template <int BR, int NS, int WCO = 2, int WKC = 2>
+__global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_v3_kernel(const WgradArgs a) {
+    constexpr int NW = WCO * WKC;
+    constexpr int TCO = 64 * WCO, TK = 64 * WKC;
+    constexpr int NSD = (TCO + 127) / 128, NSX = (TK + 127) / 128;  // 128-channel sub-images per operand
+    constexpr int SI = BR * 256;          // bytes of one sub-image per stage
+    constexpr int SBD = NSD * SI, SBX = NSX * SI;
+    constexpr int PD = NSD * (BR / 4) / NW, PX = NSX * (BR / 4) / NW;  // 1-KB pieces per wave per stage
+    static_assert(PD >= 1 && PX >= 1 && PD * NW == NSD * (BR / 4) && PX * NW == NSX * (BR / 4), "piece split");
+    constexpr int LPS = PD + PX;          // DMA instructions per wave per stage
     constexpr int NKS = BR / 32;          // MFMA k-steps per stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sD = smem;
-    char* sX = smem + NS * SB;
+    char* sX = smem + NS * SBD;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wco = wid & 1, wkc = wid >> 1;
+    const int wco = wid % WCO, wkc = wid / WCO;
     const int K = a.KH * a.KW * a.Ci;
-    const int nco = (a.Co + 127) / 128, nkc = (K + 127) / 128;  // (Co / K = 64: one half-used tile, wgrad_v3_ok)
+    const int nco = (a.Co + TCO - 1) / TCO, nkc = (K + TK - 1) / TK;  // (Co / K = 64: one half-used tile, wgrad_v3_ok)
     const int ntiles = nco * nkc;
     const int lid = xcd_remap(blockIdx.x, gridDim.x);
     const int tile = lid % ntiles, split = lid / ntiles;
-    const int co0 = (tile % nco) * 128, kc0 = (tile / nco) * 128;
+    const int co0 = (tile % nco) * TCO, kc0 = (tile / nco) * TK;
     const int mbeg = split * a.m_per_split;
     if (mbeg >= a.M) return;
     const int mend = min(a.M, mbeg + a.m_per_split);
@@ -79,15 +88,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
     const __amdgpu_buffer_rsrc_t rx = wg3_rsrc(
         a.X + xro + ci0, (uint32_t)min(((size_t)a.N * a.H * a.W * a.Ci - xro - ci0) * 2, (size_t)0x7FFFFFFF));
 
-    // this lane's DMA slot: row (within the 4-row piece) and source chunk
+    // this lane's DMA slots: piece j of an operand = sub-image j / (BR / 4), rows 4 (j % (BR / 4)) .. + 3; the lane
+    // takes row + prow and source chunk (lane & 15) ^ swz(row) of the sub-image's 128 channels
     const int prow = lane >> 4;
-    uint32_t voffd[PPW], rowcs[PPW];
+    uint32_t voffd[PD], rowx[PX], colx[PX];
 #pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-        const int r = (wid * PPW + q) * 4 + prow;  // row within the stage
-        const int ch = (lane & 15) ^ wg3_swz(r);
-        rowcs[q] = (uint32_t)(ch * 16);
-        voffd[q] = (uint32_t)(r * a.Co * 2) + rowcs[q];
+    for (int q = 0; q < PD; ++q) {
+        const int j = wid * PD + q, h = j / (BR / 4);
+        const int r = (j % (BR / 4)) * 4 + prow;
+        voffd[q] = (uint32_t)(r * a.Co * 2 + h * 256 + (((lane & 15) ^ wg3_swz(r)) << 4));
+    }
+#pragma unroll
+    for (int q = 0; q < PX; ++q) {
+        const int j = wid * PX + q, h = j / (BR / 4);
+        const int r = (j % (BR / 4)) * 4 + prow;
+        rowx[q] = (uint32_t)r;
+        colx[q] = (uint32_t)(h * 256 + (((lane & 15) ^ wg3_swz(r)) << 4));
     }
     const uint32_t dstep = (uint32_t)(BR * a.Co * 2);
 
@@ -95,17 +111,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
     auto issue = [&]() {
         if (is >= nst) return;
         const int buf = is % NS;
-        char* dD = sD + buf * SB + wid * PPW * 1024;
-        char* dX = sX + buf * SB + wid * PPW * 1024;
+        char* dD = sD + buf * SBD + wid * PD * 1024;
+        char* dX = sX + buf * SBX + wid * PX * 1024;
         const int mb = mbeg + is * BR;
 #pragma unroll
-        for (int q = 0; q < PPW; ++q) wg3_dma(rd, dD + q * 1024, voffd[q] + (uint32_t)is * dstep);
+        for (int q = 0; q < PD; ++q) wg3_dma(rd, dD + q * 1024, voffd[q] + (uint32_t)is * dstep);
 #pragma unroll
-        for (int q = 0; q < PPW; ++q) {
-            const int m = mb + (wid * PPW + q) * 4 + prow;
+        for (int q = 0; q < PX; ++q) {
+            const int m = mb + (int)rowx[q];
             uint32_t off = WG3_OOB;
             if (dense) {
-                if (m < mend) off = (uint32_t)(m - mbeg) * (uint32_t)(a.Ci * 2) + rowcs[q];
+                if (m < mend) off = (uint32_t)(m - mbeg) * (uint32_t)(a.Ci * 2) + colx[q];
             } else if (m < mend) {
                 const uint32_t img = fdiv((uint32_t)m, a.mg_ohw, a.sh_ohw);
                 const uint32_t rem = (uint32_t)m - img * (uint32_t)ohw;
@@ -114,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
                 const int ih = (int)oh * a.stride + dh, iw = (int)ow * a.stride + dw;
                 if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
                     off = (((img - (uint32_t)img0) * (uint32_t)a.H + (uint32_t)ih) * (uint32_t)a.W + (uint32_t)iw) *
-                              (uint32_t)(a.Ci * 2) + rowcs[q];
+                              (uint32_t)(a.Ci * 2) + colx[q];
             }
             wg3_dma(rx, dX + q * 1024, off);
         }
@@ -131,17 +147,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
 
     // transposed-read addressing: group g = lane >> 4 reads rows R1 + q and R1 + 16 + q
     // (R1 = (g & 1) * 8 + (g >> 1) * 4: a 32-lane half's two blocks 8 rows apart), columns
-    // c0 + 4p .. +3 of chunk (c0 / 8 + (p >> 1)) ^ swz(row), byte 8 * (p & 1)
+    // c0 + 4p .. +3 of chunk (c0 / 8 + (p >> 1)) ^ swz(row), byte 8 * (p & 1); the wave's 64 columns are half
+    // (wco & 1) of sub-image wco >> 1
     const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
     const int r1 = (g & 1) * 8 + (g >> 1) * 4 + q4, r2 = r1 + 16;
     int offa[4][2], offb[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int ca = wco * 8 + 2 * i + (p4 >> 1), cb = wkc * 8 + 2 * i + (p4 >> 1);
-        offa[i][0] = r1 * 256 + ((ca ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
-        offa[i][1] = r2 * 256 + ((ca ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
-        offb[i][0] = r1 * 256 + ((cb ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
-        offb[i][1] = r2 * 256 + ((cb ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
+        const int ca = (wco & 1) * 8 + 2 * i + (p4 >> 1), cb = (wkc & 1) * 8 + 2 * i + (p4 >> 1);
+        const int sa = (wco >> 1) * SI, sb = (wkc >> 1) * SI;
+        offa[i][0] = sa + r1 * 256 + ((ca ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
+        offa[i][1] = sa + r2 * 256 + ((ca ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
+        offb[i][0] = sb + r1 * 256 + ((cb ^ wg3_swz(r1)) << 4) + 8 * (p4 & 1);
+        offb[i][1] = sb + r2 * 256 + ((cb ^ wg3_swz(r2)) << 4) + 8 * (p4 & 1);
     }
 
     for (int s = 0; s < nst; ++s) {
@@ -153,8 +171,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_v3_kernel(const WgradArgs a) {
         __builtin_amdgcn_s_barrier();
         issue();
         const int buf = s % NS;
-        const char* bD = sD + buf * SB;
-        const char* bX = sX + buf * SB;
+        const char* bD = sD + buf * SBD;
+        const char* bX = sX + buf * SBX;
         if (kc0 + wkc * 64 >= K || co0 + wco * 64 >= a.Co) continue;  // (wave-uniform) past K / Co: never computed
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
@@ -206,15 +224,22 @@ bool wgrad_v3_ok(const WgradArgs& a) {
     return true;
 }
 
-template <int BR, int NS>
+// the wide tiles cover whole tiles only (one filter tap per k tile: Ci % TK == 0)
+template <int WCO, int WKC>
+bool wgrad_v3w_ok(const WgradArgs& a) {
+    return wgrad_v3_ok(a) && a.Co % (64 * WCO) == 0 && a.Ci % (64 * WKC) == 0;
+}
+
+template <int BR, int NS, int WCO = 2, int WKC = 2>
 int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
+    constexpr int TCO = 64 * WCO, TK = 64 * WKC;
     const int K = a.KH * a.KW * a.Ci;
-    const int ntiles = ((a.Co + 127) / 128) * ((K + 127) / 128);
+    const int ntiles = ((a.Co + TCO - 1) / TCO) * ((K + TK - 1) / TK);
     if (splits <= 0) {
-        // one wave of 2 blocks per CU over 256 CUs: the 1x1 wgrads are split-K streams whose second, partial
-        // wave of blocks cost more than the extra atomics of deeper splits save (same-box bench: 512 blocks
-        // 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282)
-        constexpr int target = 512;
+        // one wave of blocks over 256 CUs (two per CU for the 4-wave tile): the 1x1 wgrads are split-K streams whose
+        // second, partial wave of blocks cost more than the extra atomics of deeper splits save (same-box bench:
+        // 512 blocks 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282)
+        constexpr int target = WCO * WKC == 4 ? 512 : 256;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));
@@ -227,8 +252,8 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
         mps = (mps / 2 + BR - 1) / BR * BR;
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
-    const size_t lds = (size_t)NS * 2 * BR * 256;
-    hipLaunchKernelGGL((wgrad_v3_kernel<BR, NS>), dim3(ntiles * splits), dim3(256), lds, st, a);
+    const size_t lds = (size_t)NS * ((TCO + 127) / 128 + (TK + 127) / 128) * BR * 256;
+    hipLaunchKernelGGL((wgrad_v3_kernel<BR, NS, WCO, WKC>), dim3(ntiles * splits), dim3(WCO * WKC * 64), lds, st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;

@@ -212,6 +212,26 @@ def test_wgrad_v3(shape, variant):
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
 
 
+@pytest.mark.parametrize("variant", [6])
+@pytest.mark.parametrize("shape", [(3, 256, 11, 256, 1, 1, 0), (2, 256, 10, 512, 1, 2, 0), (2, 512, 7, 256, 3, 1, 1),
+                                   (2, 256, 9, 768, 1, 1, 0), (1, 256, 5, 512, 3, 2, 1)])
+def test_wgrad_v3_wide(shape, variant):
+    """The wide wgrad_v3 tile (256 x 256 on 16 waves, one block per CU, staged as 128-channel sub-images) against
+    the fp32 conv weight gradient; 1x1 dense / strided and 3x3 with borders, ragged M, explicit split-K."""
+    from imagent_amd.ops.conv import igemm_wgrad
+    N, Ci, H, Co, k, s, p = shape
+    torch.manual_seed(7)
+    x = bf(torch.randn(N, Ci, H, H, device=DEV))
+    w = torch.randn(Co, Ci, k, k, device=DEV).requires_grad_(True)
+    yr = F.conv2d(x.float(), w, None, s, p)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    for splits in (0, 3):
+        dw = torch.zeros(Co, k, k, Ci, device=DEV)
+        igemm_wgrad(nhwc(g), nhwc(x), dw, s, p, k, k, splits=splits, variant=variant)
+        assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
+
+
 @pytest.mark.parametrize("N,Ci,Co,H,W", [(3, 64, 64, 56, 56), (5, 64, 64, 8, 56), (1, 64, 64, 4, 56),
                                          (3, 128, 128, 28, 28), (2, 64, 192, 8, 28), (2, 256, 256, 14, 14),
                                          (3, 128, 64, 14, 14), (3, 512, 512, 7, 7), (1, 64, 128, 7, 7)])
