@@ -841,7 +841,11 @@ int conv_stream(const IGemmArgs& a, hipStream_t st, int bn) {
     // weight slices resident in LDS (as the K = 256 forwards) instead of the one-tile-per-block v3 loop, whose
     // 4-stage main loop leaves these epilogue-heavy GEMMs latency-bound (-20 % per call, round 4)
     if (a.C == 256 && (a.flags & IG_BNBWD) && a.Nout > 128) {
-        if (bn_hint == 128 && !a.bnx2 && a.Nout % 128 == 0)  // (tile 21: A/B)
+        // 128-channel slices (half the slices re-reading each pixel group): in-step A/B at 2048 img 16,622 / 16,663
+        // vs 16,530 / 16,522 img/s with 64 (1024 -> 256 @14 dgrad + BN backward 705 -> 488 us, 512 -> 256 @28
+        // 1460 -> 1033; at 1024 img round 5 they had measured even); tile 22 forces 64. The second-BN-branch form
+        // stays on 64 (at 128 it spills 96 B: in-step 16,604 / 16,651 vs 16,662 / 16,653)
+        if (bn_hint != 64 && a.Nout % 128 == 0 && !a.bnx2)
             return a.bnym ? launch_stream1<256, 128, 2, 1>(a, st) : launch_stream1<256, 128, 2, 2>(a, st);
         if (a.bnx2) return a.bnym ? launch_stream1<256, 64, 2, 3>(a, st) : 1;
         return a.bnym ? launch_stream1<256, 64, 2, 1>(a, st) : launch_stream1<256, 64, 2, 2>(a, st);

@@ -48,6 +48,7 @@ SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _sh
 BENCH_KERNELS = [
     "conv_stream_kernel<128, 128, 2, 1, false, false, 0>",
     "conv_stream_kernel<128, 128, 2, 3, false, false, 0>",
+    "conv_stream_kernel<256, 128, 2, 1, false, false, 0>",
     "conv_stream_kernel<256, 64, 2, 0, false, false, 0>",
     "conv_stream_kernel<256, 64, 2, 1, false, false, 0>",
     "conv_stream_kernel<256, 64, 2, 3, false, false, 0>",
@@ -69,7 +70,7 @@ BENCH_KERNELS = [
     "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
     "wgrad_kernel<64, 128, 1, true, 4, 32, false>",
-    "wgrad_v3_kernel<64, 2>",
+    "wgrad_v3_kernel<64, 2, 2, 2>",
 ]
 
 
