@@ -171,7 +171,8 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
         // (the fused BN-backward dgrads on 128x128 tiles with their epilogue operands prefetched instead: within
-        // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken)
+        // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken; again at 2048 img in round 5, isolated
+        // 2-7 % faster, in-step 16,584 / 16,576 vs 16,612 / 16,621 img/s)
         if (a.Nout >= V3_BIG_MIN_N && t8 >= 192 && K >= V3_BIG_MIN_K) {
             const int i1 = tail_split_images(a);
             if (i1 > 0) {  // whole rounds of 256x256 tiles, the remaining images as 128x128 tiles
