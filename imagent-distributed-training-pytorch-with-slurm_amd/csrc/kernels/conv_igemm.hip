@@ -167,6 +167,8 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
             case 27: return launch_v3<256, 256, 2, 2, 8, 128, 2, 0, true>(a, st);
             default: return launch_v3<128, 128, 2, 2, 4, 128, 2, 0, true>(a, st);
         }
+        // (a 16-wave 256x256 tile of 64 x 64 waves, round 5: no faster than these on any R50 shape, its staged BN-backward
+        // epilogue 1.4-1.7x slower from spills at 128 VGPRs -- not kept)
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
