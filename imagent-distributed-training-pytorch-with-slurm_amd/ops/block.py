@@ -65,6 +65,11 @@ _GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
 # loses (same-box A/B: ResNet-152 at 256 img/GPU 4,699 img/s with every block in the Gram form vs 5,080 without,
 # at 1024 img/GPU 6,279 vs 6,019; ResNet-50 at 256 11,636 vs 12,097)
 _GRAM_MIN_ROWS = int(os.environ.get("IMAGENT_GRAM_MIN_ROWS", "100000"))
+# ... and bottleneck widths p <= 256: the extension grows as p^2 M against ~32 M p bytes saved, and at p = 512
+# (ResNet-50's layer 4) it loses at the same per-block work where p = 256 wins (same-box A/B at 2048 img/GPU, where
+# layer 4 passes the row bound: 16,620 / 16,610 img/s without its Gram form vs 16,543 / 16,529 with it; layer 3 at
+# 1024 img, the same M p, is a round-4 win)
+_GRAM_MAX_P = 256
 # ... and in identity blocks bn3's FORWARD too: its batch statistics come from h2 (mean = W3 colsum(h2) / M,
 # E[x3^2] = rowsum(W3 G * W3) / M with the Gram matrix G the weight gradient needs anyway), so conv3's epilogue
 # applies bn3 + shortcut + ReLU and writes the block output and its mask bits: x3 is never written or read
@@ -85,7 +90,8 @@ def _gram_ok(block, q, x) -> bool:
     s = pairs[1][0].stride  # the bottleneck's stride sits in conv2
     rows = x.shape[0] * (x.shape[1] // s) * (x.shape[2] // s)
     return (c3.kh == 1 and c3.kw == 1 and c3.stride == 1 and c3.padding == 0 and c3.in_channels % 64 == 0
-            and c3.out_channels % 64 == 0 and rows >= _GRAM_MIN_ROWS)
+            and c3.out_channels % 64 == 0 and rows >= _GRAM_MIN_ROWS
+            and (c3.in_channels <= _GRAM_MAX_P or _GRAM_MIN_ROWS == 0))
 
 
 def _xfuse_ok(conv, a, q) -> bool:
