@@ -339,6 +339,9 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     // 2 % slower than this register-staged loop on every R50 shape: not kept)
     // (launch<256, 256, 2, false, 8> -- one 8-wave block per CU -- measured 23 %
     // slower in total: this register-staged loop needs two blocks per CU)
+    // (round 5, 2048 img, 3x3 stride 2 / 7x7: the LDS-DMA loop waits on its fills -- SQ_WAIT_ANY 44 % of wave
+    // cycles vs 22 % here, scripts/pmc_wgrad.sh; deeper rings cost blocks per CU and run slower still, 32-row
+    // stages x 2 at four blocks per CU come within 4 % on 512 @7 and stay 5-15 % behind on the stride-2 shapes)
     return launch<128, 128, 2, false>(a, splits, st);
 }
 

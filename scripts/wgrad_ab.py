@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--variants", default="0,-1,1,2,4,9")
     ap.add_argument("--set", default="default", choices=["default", "1x1"])
+    ap.add_argument("--only", default=None, help="Ci,H,Co,k,s of one shape")
+    ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     from imagent_amd.ops.conv import igemm_wgrad
     dev = "cuda"
@@ -33,6 +35,8 @@ def main():
     print("   Ci    H   Co k s | n | " + " | ".join(f"v{v:>3} us" for v in variants))
     tot = [0.0] * len(variants)
     for ci, h, co, k, s, n in (SHAPES_1X1 if a.set == "1x1" else SHAPES):
+        if a.only and tuple(int(v) for v in a.only.split(",")) != (ci, h, co, k, s):
+            continue
         oh = (h + 2 * (k // 2) - k) // s + 1
         x = torch.randn(a.batch, h, h, ci, device=dev).to(torch.bfloat16)
         dy = torch.randn(a.batch, oh, oh, co, device=dev).to(torch.bfloat16)
@@ -49,7 +53,7 @@ def main():
                     ref = dw.clone()
                 err = ((dw - ref).norm() / ref.norm()).item()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                reps = 10
+                reps = a.reps
                 e0.record()
                 for _ in range(reps):
                     igemm_wgrad(dy, x, dw, s, k // 2, k, k, variant=v)
