@@ -77,6 +77,12 @@ def main():
     from imagent_amd.ops.conv import conv_out_size, igemm_dgrad, igemm_fwd, igemm_wgrad
     dev = "cuda"
     tot = collections.defaultdict(float)
+    # clock ramp: the first ~second of GPU work runs 10-15 % slower (round-5 A/Bs timed the first config slowest),
+    # so spin the GPU before the first timed call
+    _a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    for _ in range(200):
+        _a = _a @ _a.T * 1e-4
+    torch.cuda.synchronize()
     rows = []
     print(f"{'Ci':>5} {'H':>4} {'Co':>5} k s | cnt | {'fwd us':>8} {'TF':>6} {'roof':>6} | {'dgrad':>8} {'TF':>6} | "
           f"{'wgrad':>8} {'TF':>6}" + (" | miopen fwd" if a.miopen else ""))

@@ -31,6 +31,12 @@ def main():
     a = ap.parse_args()
     from imagent_amd.ops.conv import igemm_wgrad
     dev = "cuda"
+    # clock ramp: the first ~second of GPU work runs 10-15 % slower (round-5 A/Bs timed the first config slowest),
+    # so spin the GPU before the first timed call
+    _a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    for _ in range(200):
+        _a = _a @ _a.T * 1e-4
+    torch.cuda.synchronize()
     variants = [int(v) for v in a.variants.split(",")]
     print("   Ci    H   Co k s | n | " + " | ".join(f"v{v:>3} us" for v in variants))
     tot = [0.0] * len(variants)
