@@ -251,6 +251,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? (BR == 32 ? 3 : 2) : 1) void wgr
 }  // namespace
 
 #include "conv_wgrad_v3.h"
+#include "conv_wgrad_stem.h"
 #include "conv_wgrad_halo.h"
 
 namespace {
@@ -308,6 +309,9 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     if ((a.stem & 1) && a.xbn) return -110;
     if (a.stem & 1) {
         if (a.Ci != 4 || a.KW > 8 || a.Co % 8) return -102;
+        // the 224-px 7x7 stem: the band kernel (conv_wgrad_stem.h; in-step 16,856 / 16,883 vs 16,738 / 16,756 img/s
+        // with the register-staged stem loop below, same box)
+        if (stem_wgrad_band_ok(a)) return launch_stem_wgrad_band(a, st);
         return launch<64, 128, 1, true>(a, splits, st);
     }
     if (a.Ci % 8 || a.Co % 8) return -100;
@@ -345,14 +349,18 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     return launch<128, 128, 2, false>(a, splits, st);
 }
 
-// explicit kernel choice (tests, A/B): -1 the register-staged kernel, 1..4 the v3 variants of
-// IMAGENT_WGRAD_V3 (-106 when the shape is not one v3 covers), 9 the halo-tiled 64 -> 64 3x3 kernel,
-// 0 the default dispatch
+// explicit kernel choice (tests, A/B): -1 the register-staged kernel, -2 the stem's register-staged kernel, 1..4
+// the v3 variants of IMAGENT_WGRAD_V3 and 6 its 256 x 256 tile (-106 when the shape is not one v3 covers), 9 the
+// halo-tiled 64 -> 64 3x3 kernel, 0 the default dispatch (the band kernel for the 224-px stem)
 IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int variant, void* stream) {
     const WgradArgs& a = *args;
     if (variant == 0) return imk_conv_wgrad(args, splits, stream);
     if (a.M <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    if (variant == -2) {  // the stem's register-staged kernel (A/B against the band kernel)
+        if (!(a.stem & 1) || a.Ci != 4 || a.KW > 8 || a.Co % 8) return -106;
+        return launch<64, 128, 1, true>(a, splits, st);
+    }
     if (variant < 0) {
         if (a.stem || a.xbn || a.Ci % 8 || a.Co % 8) return -106;
         return a.Co <= 64 ? launch<64, 128, 1, false>(a, splits, st) : launch<128, 128, 2, false>(a, splits, st);

@@ -338,7 +338,7 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     """dw[Co, KH*KW*Ci] (fp32, contiguous rows) += wgrad(dy[N,OH,OW,Co], x[N,H,W,Ci]).
     ``stem``: x has 4 channels, dw is ``[Co][KH][32]`` (see :func:`igemm_fwd`).
     ``xbn``: the X operand is relu(x * xbn[0] + xbn[1]) (1x1 convs; as in :func:`igemm_fwd`).
-    ``variant`` (tests / A/B): 0 the default dispatch, -1 the register-staged kernel, 1..4 and 6 the
+    ``variant`` (tests / A/B): 0 the default dispatch, -1 the register-staged kernel (-2: the stem's), 1..4 and 6 the
     LDS-DMA v3 kernel's stage shapes (conv_wgrad_v3.h)."""
     N, H, W, Ci = x.shape
     _, OH, OW, Co = dy.shape

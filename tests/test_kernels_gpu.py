@@ -212,6 +212,28 @@ def test_wgrad_v3(shape, variant):
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
 
 
+@pytest.mark.parametrize("N", [3, 12])
+def test_stem_wgrad_band(N):
+    """The 7x7 / stride-2 stem's band weight gradient (conv_wgrad_stem.h: dY and the input rows of a band staged in
+    LDS, both operands by transposing reads, per-block accumulators) against the fp32 conv weight gradient and the
+    register-staged stem kernel (variant -2); N = 12 gives 672 bands, more than one per resident block."""
+    from imagent_amd.ops.conv import igemm_wgrad
+    torch.manual_seed(5)
+    x = torch.zeros(N, 224, 224, 4, device=DEV)
+    x[..., :3] = torch.randn(N, 224, 224, 3, device=DEV)
+    x = bf(x)
+    w = torch.randn(64, 4, 7, 7, device=DEV).requires_grad_(True)
+    yr = F.conv2d(nchw(x).float(), w, None, 2, 3)
+    g = bf(torch.randn_like(yr))
+    yr.backward(g.float())
+    ref = w.grad.permute(0, 2, 3, 1)  # [co][kh][kw][ci]
+    for variant in (0, -2):
+        dw = torch.zeros(64, 7, 32, device=DEV)
+        igemm_wgrad(nhwc(g), x, dw, 2, 3, 7, 7, stem=True, variant=variant)
+        got = dw[:, :, :28].reshape(64, 7, 7, 4)
+        assert rel(got, ref) < 5e-3, variant
+
+
 @pytest.mark.parametrize("variant", [6])
 @pytest.mark.parametrize("shape", [(3, 256, 11, 256, 1, 1, 0), (2, 256, 10, 512, 1, 2, 0), (2, 512, 7, 256, 3, 1, 1),
                                    (2, 256, 9, 768, 1, 1, 0), (1, 256, 5, 512, 3, 2, 1)])
