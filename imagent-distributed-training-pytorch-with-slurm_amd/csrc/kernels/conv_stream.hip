@@ -735,6 +735,8 @@ bool stem_band_ok(const IGemmArgs& a) {
 }
 
 int launch_stem_band(const IGemmArgs& a, hipStream_t st) {
+    // R = 4 output rows per band (2048 img: 1,205 us; R = 2 1,391, R = 6 1,344 and R = 8 2,258 spill -- the 28 weight
+    // fragments held in registers leave no room for a taller band's prefetch)
     constexpr int R = 4;
     const size_t lds = 2 * (size_t)(2 * R + 5) * 232 * 8 + 4 * 16 * 64 * 2;
     static int resident = 0;
