@@ -382,4 +382,24 @@ IMK_EXPORT int imk_conv_wgrad_variant(const WgradArgs* args, int splits, int var
     }
 }
 
+// G += h2^T h2 for an [M][p] bf16 h2 (the Gram-form bottleneck's Gram matrix, ops/bn_gram.py), p = 64 / 128, G fp32
+// [p][p] accumulated: the v3 weight-gradient loop with ONE staged operand (SYM 1), for p = 64 on h2 viewed as
+// [M / 2][128] pixel pairs whose Gram matrix's two diagonal quadrants sum to G (SYM 2). -106: not a shape this covers
+IMK_EXPORT int imk_gram_sym(const void* h2, float* G, long M, int p, int splits, void* stream) {
+    if ((p != 64 && p != 128) || M <= 0 || (p == 64 && M % 2)) return -106;
+    WgradArgs a{};
+    a.dY = a.X = static_cast<const bf16_t*>(h2);
+    a.dW = G;
+    const long rows = p == 64 ? M / 2 : M;
+    if (rows > 0x7FFFFFFF) return -106;
+    a.N = (int)rows;
+    a.H = a.W = a.OH = a.OW = 1;
+    a.M = (int)rows;
+    a.Ci = a.Co = 128;
+    a.KH = a.KW = a.stride = 1;
+    a.pad = 0;
+    hipStream_t st = (hipStream_t)stream;
+    return p == 64 ? launch_wgrad_v3<64, 2, 2, 2, 2>(a, splits, st) : launch_wgrad_v3<64, 2, 2, 2, 1>(a, splits, st);
+}
+
 IMK_EXPORT int imk_wgrad_args_size() { return (int)sizeof(WgradArgs); }

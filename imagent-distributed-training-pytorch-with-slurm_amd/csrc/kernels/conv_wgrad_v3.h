@@ -44,8 +44,13 @@ __device__ __forceinline__ int wg3_swz(int row) { return ((row & 3) << 2) | ((ro
 // half the operand bytes per MFMA FLOP -- the L2 -> LDS path, not the MFMA, bounds the 128 x 128 tile. A tile
 // wider than 128 channels is staged as 128-channel sub-images of the same 256-B-row layout (sub-image h: channels
 // 128 h .. 128 h + 127 of every row of the stage), so the DMA pieces and the transposed reads are unchanged.
-template <int BR, int NS, int WCO = 2, int WKC = 2>
+// SYM (the Gram matrix G = h2^T h2 of a Gram-form bottleneck, bn_gram.hip, X == dY): 1 -- one operand staged once and
+// read as both fragments; 2 -- a 64-channel h2 viewed as [M / 2][128] rows of pixel PAIRS, whose 128 x 128 Gram
+// matrix holds G in its two diagonal quadrants (even pixels + odd pixels): only the two diagonal waves compute, both
+// adding into the same 64 x 64 output (row pitch 64)
+template <int BR, int NS, int WCO = 2, int WKC = 2, int SYM = 0>
 __global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_v3_kernel(const WgradArgs a) {
+    static_assert(SYM == 0 || (WCO == 2 && WKC == 2), "symmetric forms: the 128 x 128 tile");
     constexpr int NW = WCO * WKC;
     constexpr int TCO = 64 * WCO, TK = 64 * WKC;
     constexpr int NSD = (TCO + 127) / 128, NSX = (TK + 127) / 128;  // 128-channel sub-images per operand
@@ -53,11 +58,11 @@ __global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_
     constexpr int SBD = NSD * SI, SBX = NSX * SI;
     constexpr int PD = NSD * (BR / 4) / NW, PX = NSX * (BR / 4) / NW;  // 1-KB pieces per wave per stage
     static_assert(PD >= 1 && PX >= 1 && PD * NW == NSD * (BR / 4) && PX * NW == NSX * (BR / 4), "piece split");
-    constexpr int LPS = PD + PX;          // DMA instructions per wave per stage
+    constexpr int LPS = SYM ? PD : PD + PX;  // DMA instructions per wave per stage
     constexpr int NKS = BR / 32;          // MFMA k-steps per stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* sD = smem;
-    char* sX = smem + NS * SBD;
+    char* sX = SYM ? smem : smem + NS * SBD;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_
 #pragma unroll
         for (int q = 0; q < PD; ++q) wg3_dma(rd, dD + q * 1024, voffd[q] + (uint32_t)is * dstep);
 #pragma unroll
-        for (int q = 0; q < PX; ++q) {
+        for (int q = 0; q < (SYM ? 0 : PX); ++q) {
             const int m = mb + (int)rowx[q];
             uint32_t off = WG3_OOB;
             if (dense) {
@@ -174,6 +179,7 @@ __global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_
         const char* bD = sD + buf * SBD;
         const char* bX = sX + buf * SBX;
         if (kc0 + wkc * 64 >= K || co0 + wco * 64 >= a.Co) continue;  // (wave-uniform) past K / Co: never computed
+        if (SYM == 2 && wco != wkc) continue;                           // off-diagonal quadrant of the pair Gram
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             bf16x8 fd[4], fx[4];
@@ -199,6 +205,18 @@ __global__ __launch_bounds__(WCO * WKC * 64, WCO * WKC == 4 ? 2 : 1) void wgrad_
 
     // acc[i][j][r]: co = co0 + wco*64 + i*16 + (lane>>4)*4 + r ; k = kc0 + wkc*64 + j*16 + (lane&15)
     if (kc0 + wkc * 64 >= K || co0 + wco * 64 >= a.Co) return;
+    if constexpr (SYM == 2) {
+        if (wco != wkc) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float* dst = a.dW + (size_t)(i * 16 + (lane >> 4) * 4 + r) * 64 + (lane & 15);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) atomicAdd(dst + j * 16, acc[i][j][r]);
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -230,7 +248,7 @@ bool wgrad_v3w_ok(const WgradArgs& a) {
     return wgrad_v3_ok(a) && a.Co % (64 * WCO) == 0 && a.Ci % (64 * WKC) == 0;
 }
 
-template <int BR, int NS, int WCO = 2, int WKC = 2>
+template <int BR, int NS, int WCO = 2, int WKC = 2, int SYM = 0>
 int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
     constexpr int TCO = 64 * WCO, TK = 64 * WKC;
     const int K = a.KH * a.KW * a.Ci;
@@ -252,8 +270,8 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
         mps = (mps / 2 + BR - 1) / BR * BR;
     splits = (a.M + mps - 1) / mps;
     a.m_per_split = mps;
-    const size_t lds = (size_t)NS * ((TCO + 127) / 128 + (TK + 127) / 128) * BR * 256;
-    hipLaunchKernelGGL((wgrad_v3_kernel<BR, NS, WCO, WKC>), dim3(ntiles * splits), dim3(WCO * WKC * 64), lds, st, a);
+    const size_t lds = (size_t)NS * ((TCO + 127) / 128 + (SYM ? 0 : (TK + 127) / 128)) * BR * 256;
+    hipLaunchKernelGGL((wgrad_v3_kernel<BR, NS, WCO, WKC, SYM>), dim3(ntiles * splits), dim3(WCO * WKC * 64), lds, st, a);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;

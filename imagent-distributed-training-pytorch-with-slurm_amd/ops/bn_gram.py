@@ -39,6 +39,20 @@ def _splits(co: int, ci: int) -> int:
     return max(16, 512 // ((co // 128) * (ci // 128)))
 
 
+def gram_G(h2: torch.Tensor, G: torch.Tensor) -> None:
+    """G += h2^T h2 ([p][p] fp32) on the current stream. p = 64 / 128: the weight-gradient loop with h2 staged ONCE
+    and read as both operands (imk_gram_sym; for p = 64 over pixel pairs); otherwise the plain weight gradient.
+    At 2048 img (scripts/gram_bench.py): p = 64 @56 275 -> 159 us (5.2 TB/s), p = 128 @28 116 -> 105; in-step
+    16,830 / 16,912 vs 16,840 / 16,777 img/s (same box, within noise)."""
+    p = h2.shape[-1]
+    M = h2.numel() // p
+    if p in (64, 128) and M % 2 == 0:
+        _lib.check(_lib.kernels().imk_gram_sym(h2.data_ptr(), G.data_ptr(), M, p, 512, _lib.stream_ptr()),
+                   "gram G")
+        return
+    igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
+
+
 class GramBN:
     """bn3's backward output dx3 = A g + B x3 + c, kept as (g, coef = [3][4p] (A, B, c)); T = g^T h2 when
     it was formed for the coefficients (``gram_T``)."""
@@ -135,7 +149,7 @@ def gram_fwd_stats(bn, conv, h2: torch.Tensor, s: torch.Tensor, G: torch.Tensor,
     block's shortcut-BN shift, folded into bn3's). ``P``: a zeroed [4p][p] accumulator (workspace) or None."""
     C4, p = conv.out_channels, conv.in_channels
     M = h2.numel() // p
-    igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
+    gram_G(h2, G)
     P = gram_P(conv, G, s, M, out=P)
     aff = torch.empty((2, C4), device=h2.device, dtype=torch.float32)
     w = bn.work
@@ -176,7 +190,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
                 ev = torch.cuda.Event()
                 ev.record(side)
         if P is None:
-            igemm_wgrad(h2, h2, G, 1, 0, 1, 1, splits=_splits(p, p))
+            gram_G(h2, G)
         if own_s:
             colsum_into(h2.view(-1, p), s)
         if P is None:

@@ -55,6 +55,15 @@ def main():
         line = f"{label:22s} M {M:8d} {gb:6.3f} GB |"
         t = timeit(lambda: torch.mm(dy.view(M, co).t(), x.view(M, ci)))
         line += f" mm {t:7.1f} us {gb / t * 1e3:5.2f} TB/s |"
+        if co == ci:  # the symmetric Gram path (ops/bn_gram.py gram_G)
+            from imagent_amd.ops.bn_gram import gram_G
+            out.zero_()
+            gram_G(x, out)
+            t = timeit(lambda: gram_G(x, out))
+            out.zero_()
+            gram_G(x, out)
+            e = ((out - ref).norm() / ref.norm()).item()
+            line += f" gramG {t:7.1f} us {gb / t * 1e3:5.2f} TB/s e{e:.0e} |"
         for v in variants:
             for sp in splits:
                 tag = f"v{v}" + (f"/s{sp}" if sp else "")

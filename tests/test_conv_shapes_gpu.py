@@ -70,7 +70,7 @@ BENCH_KERNELS = [
     "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
     "stem_wgrad_band_kernel<4>",
-    "wgrad_v3_kernel<64, 2, 2, 2>",
+    "wgrad_v3_kernel<64, 2, 2, 2, 0>",
 ]
 
 

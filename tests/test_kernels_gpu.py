@@ -212,6 +212,21 @@ def test_wgrad_v3(shape, variant):
         assert rel(dw.permute(0, 3, 1, 2), w.grad) < 5e-3, splits
 
 
+@pytest.mark.parametrize("p", [64, 128, 256])
+@pytest.mark.parametrize("M", [4096 * 3 + 2, 2048 * 56 * 7, 999])
+def test_gram_sym(p, M):
+    """The Gram-form bottleneck's G += h2^T h2 (ops/bn_gram.py gram_G): one staged operand read as both fragments
+    (p = 128), pixel pairs whose diagonal quadrants sum to G (p = 64), the plain weight gradient otherwise / for odd M;
+    against fp32, and accumulating into G."""
+    from imagent_amd.ops.bn_gram import gram_G
+    torch.manual_seed(3)
+    h2 = bf(torch.randn(M, 1, 1, p, device=DEV) + 0.5)  # (NHWC, as the model holds it)
+    ref = h2.view(M, p).float().t() @ h2.view(M, p).float()
+    G = torch.ones(p, p, device=DEV)
+    gram_G(h2, G)
+    assert rel(G - 1.0, ref) < 2e-4  # (fp32 sums over up to 8e5 rows in two different orders)
+
+
 @pytest.mark.parametrize("N", [3, 12])
 def test_stem_wgrad_band(N):
     """The 7x7 / stride-2 stem's band weight gradient (conv_wgrad_stem.h: dY and the input rows of a band staged in
