@@ -402,4 +402,13 @@ IMK_EXPORT int imk_gram_sym(const void* h2, float* G, long M, int p, int splits,
     return p == 64 ? launch_wgrad_v3<64, 2, 2, 2, 2>(a, splits, st) : launch_wgrad_v3<64, 2, 2, 2, 1>(a, splits, st);
 }
 
+// the stem's weight gradient with its BatchNorm's backward apply fused in (conv_wgrad_stem.h BNX): dY = g, the ReLU-
+// masked maxpool-backward gradient; bnx = the BN input; coef [3][64] = (A, B, c) of imk_bn_bwd_coef. -106: not the
+// band kernel's shape
+IMK_EXPORT int imk_stem_wgrad_bnx(const WgradArgs* args, const void* bnx, const float* coef, void* stream) {
+    const WgradArgs& a = *args;
+    if (!stem_wgrad_band_ok(a) || !bnx || !coef || a.OH % 2) return -106;
+    return launch_stem_wgrad_band_bnx(a, (hipStream_t)stream, static_cast<const bf16_t*>(bnx), coef);
+}
+
 IMK_EXPORT int imk_wgrad_args_size() { return (int)sizeof(WgradArgs); }

@@ -32,8 +32,13 @@ constexpr int SWG_SP = (SWG_W + 8) * 8;  // staged input row pitch, bytes (colum
 
 __device__ __forceinline__ int swg_swz(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
 
-template <int R>
-__global__ __launch_bounds__(256, 2) void stem_wgrad_band_kernel(const WgradArgs a, int nbands) {
+// BNX: the stem BatchNorm's backward apply fused into the staging -- a.dY is the ReLU-masked upstream gradient g
+// (maxpool backward), bnx the BN input x, coef [3][64] = (A, B, c): the staged dY is bf16(A g + B x + c), what the
+// apply pass would have stored, so the apply pass (read g and x, write dx) disappears
+template <int R, bool BNX = false>
+__global__ __launch_bounds__(256, 2) void stem_wgrad_band_kernel(const WgradArgs a, int nbands,
+                                                                 const bf16_t* __restrict__ bnx,
+                                                                 const float* __restrict__ coef) {
     constexpr int KH = 7;
     constexpr int PR = 2 * R + KH - 2;       // staged input rows per band
     constexpr int XB = PR * SWG_SP;          // X bytes in LDS
@@ -53,7 +58,18 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_band_kernel(const WgradArgs
 
     for (int e = tid; e < XB / 16; e += 256) reinterpret_cast<u32x4*>(smem)[e] = u32x4{0u, 0u, 0u, 0u};
 
-    u32x4 sx[XPT], sd[DPT];
+    u32x4 sx[XPT], sd[DPT], sb[BNX ? DPT : 1];
+    // BNX: this thread's 16-B chunks are always channel chunk tid & 7 (256 threads, 8 chunks per pixel row)
+    float ka[BNX ? 8 : 1], kb[BNX ? 8 : 1], kc[BNX ? 8 : 1];
+    if constexpr (BNX) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ch = (tid & 7) * 8 + j;
+            ka[j] = coef[ch];
+            kb[j] = coef[64 + ch];
+            kc[j] = coef[128 + ch];
+        }
+    }
     auto load_band = [&](int band) {  // global -> registers
         const int img = band / bpi, oy0 = (band - img * bpi) * R;
         const int iy0 = 2 * oy0 - 3;
@@ -65,11 +81,13 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_band_kernel(const WgradArgs
             sx[t] = ok ? *reinterpret_cast<const u32x4*>(a.X + (((size_t)img * a.H + iy) * SWG_W) * 4 + c16 * 8)
                        : u32x4{0u, 0u, 0u, 0u};
         }
-        const bf16_t* dy = a.dY + ((size_t)img * a.OH + oy0) * SWG_OW * 64;
+        const size_t d0 = ((size_t)img * a.OH + oy0) * SWG_OW * 64;
 #pragma unroll
         for (int t = 0; t < DPT; ++t) {
             const int e = tid + 256 * t;
-            sd[t] = e < DCH ? *reinterpret_cast<const u32x4*>(dy + (size_t)e * 8) : u32x4{0u, 0u, 0u, 0u};
+            sd[t] = e < DCH ? *reinterpret_cast<const u32x4*>(a.dY + d0 + (size_t)e * 8) : u32x4{0u, 0u, 0u, 0u};
+            if constexpr (BNX)
+                sb[t] = e < DCH ? *reinterpret_cast<const u32x4*>(bnx + d0 + (size_t)e * 8) : u32x4{0u, 0u, 0u, 0u};
         }
     };
     auto store_band = [&]() {  // registers -> LDS
@@ -86,7 +104,17 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_band_kernel(const WgradArgs
             const int e = tid + 256 * t;
             if (e < DCH) {
                 const int p = e >> 3, c = e & 7;
-                *reinterpret_cast<u32x4*>(sD + p * 128 + ((c ^ swg_swz(p)) << 4)) = sd[t];
+                u32x4 v = sd[t];
+                if constexpr (BNX) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float lo = fmaf(ka[2 * k], lo_bf(sd[t][k]), fmaf(kb[2 * k], lo_bf(sb[t][k]), kc[2 * k]));
+                        const float hi =
+                            fmaf(ka[2 * k + 1], hi_bf(sd[t][k]), fmaf(kb[2 * k + 1], hi_bf(sb[t][k]), kc[2 * k + 1]));
+                        v[k] = pack_bf2(lo, hi);
+                    }
+                }
+                *reinterpret_cast<u32x4*>(sD + p * 128 + ((c ^ swg_swz(p)) << 4)) = v;
             }
         }
     };
@@ -179,13 +207,13 @@ bool stem_wgrad_band_ok(const WgradArgs& a) {
            a.pad == 3 && a.W == SWG_W && a.OW == SWG_OW && a.OH % 4 == 0 && a.OH == (a.H + 1) / 2 && a.M > 0;
 }
 
-int launch_stem_wgrad_band(const WgradArgs& a, hipStream_t st) {
-    constexpr int R = 4;
+template <int R, bool BNX>
+int launch_stem_wgrad_band_r(const WgradArgs& a, hipStream_t st, const bf16_t* bnx, const float* coef) {
     const size_t lds = (size_t)(2 * R + 5) * SWG_SP + (size_t)R * SWG_OW * 128;
     static int resident = 0;
     if (resident == 0) {
         int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stem_wgrad_band_kernel<R>, 256, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stem_wgrad_band_kernel<R, BNX>, 256, lds) != hipSuccess ||
             per_cu < 1)
             per_cu = 1;
         (void)hipGetDevice(&dev);
@@ -193,10 +221,20 @@ int launch_stem_wgrad_band(const WgradArgs& a, hipStream_t st) {
         resident = per_cu * cus;
     }
     const int nbands = a.N * (a.OH / R);
-    hipLaunchKernelGGL((stem_wgrad_band_kernel<R>), dim3(std::min(nbands, resident)), dim3(256), lds, st, a, nbands);
+    hipLaunchKernelGGL((stem_wgrad_band_kernel<R, BNX>), dim3(std::min(nbands, resident)), dim3(256), lds, st, a, nbands,
+                       bnx, coef);
     CONV_COUNTED();
     IMK_CHECK_LAUNCH();
     return 0;
+}
+
+// R = 4 output rows per band: 80 KB of LDS, two blocks fill the CU; the fused-apply form prefetches g AND x in
+// registers, which leaves room for R = 2 only
+int launch_stem_wgrad_band(const WgradArgs& a, hipStream_t st) {
+    return launch_stem_wgrad_band_r<4, false>(a, st, nullptr, nullptr);
+}
+int launch_stem_wgrad_band_bnx(const WgradArgs& a, hipStream_t st, const bf16_t* bnx, const float* coef) {
+    return launch_stem_wgrad_band_r<2, true>(a, st, bnx, coef);
 }
 
 }  // namespace

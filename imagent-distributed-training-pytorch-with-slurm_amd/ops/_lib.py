@@ -192,6 +192,7 @@ def _declare(name: str, lib) -> None:
             "imk_bn_bwd_coef": [vp, vp, vp, vp, vp, vp, i64, i32, vp],
             "imk_bn_gram_dgrad_weights": [vp, i32, vp, vp, vp, vp, i32, i32, vp],
             "imk_bn_gram_q": [vp, i32, vp, vp, i32, i32, vp],
+            "imk_stem_wgrad_bnx": [C.POINTER(WgradArgs), vp, vp, vp],
             "imk_gram_sym": [vp, vp, i64, i32, i32, vp],
             "imk_bn_gram_wgrad_fixup": [vp, vp, vp, vp, vp, vp, i32, i32, vp],
             "imk_bn_gram_p": [vp, vp, vp, vp, i64, i32, i32, vp],

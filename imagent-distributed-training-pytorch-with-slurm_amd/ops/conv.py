@@ -340,6 +340,28 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     ``xbn``: the X operand is relu(x * xbn[0] + xbn[1]) (1x1 convs; as in :func:`igemm_fwd`).
     ``variant`` (tests / A/B): 0 the default dispatch, -1 the register-staged kernel (-2: the stem's), 1..4 and 6 the
     LDS-DMA v3 kernel's stage shapes (conv_wgrad_v3.h)."""
+    a = _wgrad_args(dy, x, dw, stride, pad, KH, KW, stem, xbn)
+    if variant:
+        _lib.check(_lib.kernels().imk_conv_wgrad_variant(C.byref(a), splits, variant, _lib.stream_ptr()),
+                   f"conv wgrad variant {variant}")
+        return
+    _wgrad_call(a, splits, _lib.stream_ptr(), "conv wgrad")
+
+
+def stem_wgrad_bnx(g: torch.Tensor, x: torch.Tensor, gp: torch.Tensor, bnx: torch.Tensor, coef: torch.Tensor,
+                   stride: int, pad: int, KH: int, KW: int) -> bool:
+    """The stem's weight gradient with its BatchNorm's backward apply fused into the operand staging
+    (conv_wgrad_stem.h): gp [Co][KH][32] += wgrad(bf16(A g + B bnx + c), x) with coef = (A, B, c) [3][Co].
+    False (nothing launched) when the band kernel does not cover the shape."""
+    a = _wgrad_args(g, x, gp, stride, pad, KH, KW, True, None)
+    r = _lib.kernels().imk_stem_wgrad_bnx(C.byref(a), bnx.data_ptr(), coef.data_ptr(), _lib.stream_ptr())
+    if r == -106:
+        return False
+    _lib.check(r, "stem wgrad (fused BN apply)")
+    return True
+
+
+def _wgrad_args(dy, x, dw, stride, pad, KH, KW, stem, xbn):
     N, H, W, Ci = x.shape
     _, OH, OW, Co = dy.shape
     if stem:
@@ -356,11 +378,7 @@ def igemm_wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int
     if xbn is not None:
         assert xbn.shape == (2, Ci) and xbn.dtype == torch.float32 and xbn.is_contiguous()
         a.xbn = xbn.data_ptr()
-    if variant:
-        _lib.check(_lib.kernels().imk_conv_wgrad_variant(C.byref(a), splits, variant, _lib.stream_ptr()),
-                   f"conv wgrad variant {variant}")
-        return
-    _wgrad_call(a, splits, _lib.stream_ptr(), "conv wgrad")
+    return a
 
 
 def colsum_into(x2d: torch.Tensor, out: torch.Tensor) -> None:

@@ -82,6 +82,89 @@ class BNReluPoolFn(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+class StemFn(torch.autograd.Function):
+    """The 224-px stem -- conv1 (7x7 / 2) -> bn1 -> ReLU -> maxpool -- as ONE autograd node, so that the stem BN's
+    backward apply pass never runs: the pool backward stores the ReLU-masked gradient g and reduces the BN sums
+    (as BNReluPoolFn), ``imk_bn_bwd_coef`` turns them into dx = A g + B x + c (and dgamma / dbeta), and the stem's
+    band weight gradient applies that on its operand staging (``ops.conv.stem_wgrad_bnx``) -- the stem conv's
+    input (the image) needs no gradient, so dx is never materialised (one read of g and x and one write of dx
+    less: 3 x 3.3 GB at 2048 img/GPU). Reference ops: torchvision resnet ``conv1 -> bn1 -> relu -> maxpool``
+    (/root/reference/imagenet.py:312, backward :128)."""
+
+    @staticmethod
+    def forward(ctx, img, weight, conv, bn, k, s, p):
+        from .bn import stats_finalize
+        from .conv import igemm_fwd
+        x = igemm_fwd(img, conv.w_bf16, conv.stride, conv.padding, conv.kh, conv.kw, stats=bn.work, stem=True)
+        N, H, W, Cc = x.shape
+        OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)
+        y = torch.empty((N, OH, OW, Cc), device=x.device, dtype=x.dtype)
+        idx = torch.empty((N, OH, OW, Cc), device=x.device, dtype=torch.uint8)
+        w = bn.work
+        stats_finalize(w, N * H * W)
+        _lib.check(_lib.kernels().imk_maxpool_fwd_bn(
+            x.data_ptr(), w.stats.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(), w.save.data_ptr(),
+            y.data_ptr(), idx.data_ptr(), N, H, W, Cc, OH, OW, k, s, p, bn.eps, _lib.stream_ptr()),
+            "bn + maxpool")
+        ctx.save_for_backward(img, x, idx)
+        ctx.mods = (conv, bn)
+        ctx.geom = (N, H, W, Cc, OH, OW, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import streams
+        from .conv import stem_wgrad_bnx
+        from .grad_sink import notify_ready
+        img, x, idx = ctx.saved_tensors
+        conv, bn = ctx.mods
+        N, H, W, Cc, OH, OW, k, s, p = ctx.geom
+        g = torch.empty((N, H, W, Cc), device=dy.device, dtype=torch.bfloat16)
+        w = bn.work
+        kern = _lib.kernels()
+        _lib.check(kern.imk_maxpool_bwd_bnr(
+            dy.contiguous().data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(), w.save.data_ptr(),
+            bn.weight.data_ptr(), bn.bias.data_ptr(), w.scratch.data_ptr(), N, H, W, Cc, OH, OW, k, s, p,
+            _lib.stream_ptr()), "maxpool bwd + bn reduce")
+        coef = torch.empty((3, Cc), device=dy.device, dtype=torch.float32)
+        _lib.check(kern.imk_bn_bwd_coef(w.scratch.data_ptr(), w.save.data_ptr(), bn.weight.data_ptr(),
+                                        bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(), coef.data_ptr(),
+                                        N * H * W, Cc, _lib.stream_ptr()), "stem bn bwd coef")
+        notify_ready(bn.weight)
+        notify_ready(bn.bias)
+        streams.flush_deferred()  # layer1's conv1 weight gradient (queued behind this BN's backward)
+        side = streams.side_stream(dy.device)
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(dy.device))
+        with torch.cuda.stream(side) if side is not None else _NullCtx():
+            gp = conv.grad_pad
+            ok = stem_wgrad_bnx(g, img, gp, x, coef, conv.stride, conv.padding, conv.kh, conv.kw)
+            assert ok, "StemFn needs the band stem's shape (models.native checks it)"
+            gw = conv.weight.grad
+            _lib.check(kern.imk_stem_grad_fold(gp.data_ptr(), gw.data_ptr(), gp.shape[0], conv.in_channels,
+                                               conv.kh, conv.kw, _lib.stream_ptr()), "stem grad fold")
+            notify_ready(conv.weight)
+        if side is not None:
+            streams.protect(g, img, x, coef)
+            streams.ensure_join_after_backward()
+        return None, None, None, None, None, None, None
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def stem_fused_ok(img: torch.Tensor, conv) -> bool:
+    """Does StemFn cover this stem (the band kernels' shape: 224-px 4-channel input, 7x7 / 2 / 3, 64 channels)?"""
+    return (img.dim() == 4 and img.shape[1] == 224 and img.shape[2] == 224 and img.shape[3] == 4 and
+            conv.kh == 7 and conv.kw == 7 and conv.stride == 2 and conv.padding == 3 and conv.out_channels == 64 and
+            getattr(conv, "grad_pad", None) is not None)
+
+
 def maxpool_eval(x, k, s, p):
     N, H, W, Cc = x.shape
     OH, OW = conv_out_size(H, k, s, p), conv_out_size(W, k, s, p)

@@ -44,7 +44,9 @@ SHAPES = _shapes("resnet50", 224, 1024) + [(1024, 2048, 1, 1000, 1, 1, 0)] + _sh
 # with the dispatcher. Not listed (no plain conv shape takes them; tests/test_model_gpu.py covers them against the
 # fp32 model in test_bn_gram_backward_matches_torch and test_fp8_forward_training_step[resnet50-gram]): the
 # fused-output conv3 mode conv_stream_kernel<*, *, *, 4, ...> (bn3 + shortcut + ReLU + mask bits / e4m3 copy) and
-# the Gram-form bn3 dgrad over [g | h2], conv_stream_kernel<256, 64, 2, 2, false, false, 64>.
+# the Gram-form bn3 dgrad over [g | h2], conv_stream_kernel<256, 64, 2, 2, false, false, 64>, and the stem weight
+# gradient with the stem BN's backward apply fused in, stem_wgrad_band_kernel<2, true> (ops.misc.StemFn,
+# test_model_gpu.py::test_stem_fn_matches_unfused).
 BENCH_KERNELS = [
     "conv_stream_kernel<128, 128, 2, 1, false, false, 0>",
     "conv_stream_kernel<128, 128, 2, 3, false, false, 0>",
@@ -69,7 +71,7 @@ BENCH_KERNELS = [
     "wgrad_kernel<128, 128, 2, false, 4, 32, false>",
     "wgrad_kernel<128, 128, 2, false, 4, 64, false>",
     "wgrad_kernel<64, 128, 1, false, 4, 32, false>",
-    "stem_wgrad_band_kernel<4>",
+    "stem_wgrad_band_kernel<4, false>",
     "wgrad_v3_kernel<64, 2, 2, 2, 0>",
 ]
 

@@ -438,6 +438,44 @@ def test_fused_stem_pool_backward_matches_unfused():
     assert rel(b1, b0) < 1e-3
 
 
+def test_stem_fn_matches_unfused():
+    """The 224-px stem as ONE node (StemFn: conv + BN + ReLU + maxpool; the BN backward apply fused into the band
+    weight gradient's operand staging, dx never written) vs the stem conv node + BNReluPoolFn (apply pass, then the
+    plain band weight gradient), same input and upstream gradient: same pooled output, stem weight gradient and BN
+    parameter gradients (up to the bf16 rounding of A g + B x + c in a different operation order)."""
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native import bind_native
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.conv import ConvFn
+    from imagent_amd.ops.misc import BNReluPoolFn, StemFn, normalize_u8, stem_fused_ok
+    torch.manual_seed(6)
+    m = resnet.resnet50()
+    st = bind_native(m, torch.device(DEV))
+    m.train()
+    c1, bn1 = m.conv1, m.bn1
+    img = normalize_u8(torch.randint(0, 256, (6, 224, 224, 3), dtype=torch.uint8, device=DEV), (224, 224), 4,
+                       (0.485, 0.456, 0.406), (0.229, 0.224, 0.225))
+    assert stem_fused_ok(img, c1)
+    dpool = None
+    out = []
+    for fused in (False, True):
+        _lib.zero_(st.zero_ws)
+        st.arena.G.zero_()
+        if fused:
+            y = StemFn.apply(img, c1.weight, c1, bn1, 3, 2, 1)
+        else:
+            y = BNReluPoolFn.apply(ConvFn.apply(img, c1.weight, c1, bn1.work), bn1, 3, 2, 1)
+        if dpool is None:
+            dpool = torch.randn_like(y.float()).to(torch.bfloat16)
+        y.backward(dpool)
+        torch.cuda.synchronize()
+        out.append((y.detach().float(), c1.weight.grad.clone(), bn1.weight.grad.clone(), bn1.bias.grad.clone()))
+    (y0, w0, g0, b0), (y1, w1, g1, b1) = out
+    assert torch.equal(y0, y1)
+    assert rel(g1, g0) < 1e-3 and rel(b1, b0) < 1e-3
+    assert rel(w1, w0) < 3e-3, rel(w1, w0)
+
+
 @pytest.mark.parametrize("nox,fwd", [(True, True), (True, False), (False, False)],
                          ids=["from_T_fused_fwd", "from_T", "from_slab"])
 def test_bn_gram_backward_matches_torch(monkeypatch, nox, fwd):
