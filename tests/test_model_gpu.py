@@ -459,15 +459,16 @@ def test_stem_fn_matches_unfused():
     dpool = None
     out = []
     for fused in (False, True):
-        _lib.zero_(st.zero_ws)
         st.arena.G.zero_()
-        if fused:
-            y = StemFn.apply(img, c1.weight, c1, bn1, 3, 2, 1)
-        else:
-            y = BNReluPoolFn.apply(ConvFn.apply(img, c1.weight, c1, bn1.work), bn1, 3, 2, 1)
-        if dpool is None:
-            dpool = torch.randn_like(y.float()).to(torch.bfloat16)
-        y.backward(dpool)
+        for micro in range(2):  # two micro-batches: the gradients accumulate (--accum-steps)
+            _lib.zero_(st.zero_ws)
+            if fused:
+                y = StemFn.apply(img, c1.weight, c1, bn1, 3, 2, 1)
+            else:
+                y = BNReluPoolFn.apply(ConvFn.apply(img, c1.weight, c1, bn1.work), bn1, 3, 2, 1)
+            if dpool is None:
+                dpool = torch.randn_like(y.float()).to(torch.bfloat16)
+            y.backward(dpool if micro == 0 else -0.5 * dpool)
         torch.cuda.synchronize()
         out.append((y.detach().float(), c1.weight.grad.clone(), bn1.weight.grad.clone(), bn1.bias.grad.clone()))
     (y0, w0, g0, b0), (y1, w1, g1, b1) = out
