@@ -37,6 +37,7 @@ struct PoolBnf {
     const float* beta;
     float* save;        // [2][C] mean, rstd (for the backward)
     float inv_cnt, eps;
+    bf16_t* xsel;       // optional: the BN input at each window's argmax, like y (the backward's BN sums)
 };
 
 template <int KMAX, bool BNF = false>  // KMAX > 0: k <= KMAX, windows unrolled; 0: generic k
@@ -70,10 +71,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         const bf16_t* xn = x + (size_t)n * H * W * C + ch * 8;
         float best[8];
         int bi[8];
+        uint32_t bx[8];  // BNF: the raw bf16 input at the argmax
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             best[i] = -INFINITY;
             bi[i] = 0;
+            bx[i] = 0;
         }
         auto take = [&](const u32x4& w, bool ok, int win) {
 #pragma unroll
@@ -84,8 +87,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
                     b = bf2f(f2bf(fmaxf(fmaf(b, bsc[2 * i + 1], bsh[2 * i + 1]), 0.f)));
                 }
                 // strict > keeps the first maximum (torch semantics); NaN propagates
-                if (ok && (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i]))) { best[2 * i] = a; bi[2 * i] = win; }
-                if (ok && (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1]))) { best[2 * i + 1] = b; bi[2 * i + 1] = win; }
+                if (ok && (a > best[2 * i] || (a != a && best[2 * i] == best[2 * i]))) {
+                    best[2 * i] = a;
+                    bi[2 * i] = win;
+                    bx[2 * i] = w[i] & 0xffffu;
+                }
+                if (ok && (b > best[2 * i + 1] || (b != b && best[2 * i + 1] == best[2 * i + 1]))) {
+                    best[2 * i + 1] = b;
+                    bi[2 * i + 1] = win;
+                    bx[2 * i + 1] = w[i] >> 16;
+                }
             }
         };
         if constexpr (KMAX > 0) {
@@ -128,6 +139,14 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         const size_t off = (size_t)pix * C + ch * 8;
         *reinterpret_cast<u32x4*>(y + off) = o;
         if (idx) *reinterpret_cast<u32x2*>(idx + off) = u32x2{i0, i1};
+        if constexpr (BNF) {
+            if (bnf.xsel) {
+                u32x4 xs;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xs[i] = bx[2 * i] | (bx[2 * i + 1] << 16);
+                *reinterpret_cast<u32x4*>(bnf.xsel + off) = xs;
+            }
+        }
     }
 }
 
@@ -142,6 +161,7 @@ struct PoolBnr {
     const float* gamma;
     const float* beta;
     float* slab;         // [32][3][C]
+    const bf16_t* xsel;  // quad kernel, BNR 2: the BN input at each window's argmax (maxpool_fwd_kernel BNF), like dy
 };
 
 // WMAX > 0: at most WMAX candidate windows per dimension (ceil(k/s) <= WMAX),
@@ -270,7 +290,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
 // once per input pixel (4 + 4 loads per 4 pixels instead of 16 + 16). Input
 // pixel (a, b) takes window (i + u, j + v) iff (u == 0 || a == 1) and
 // (v == 0 || b == 1), at window offset (1 + a - 2u) * 3 + (1 + b - 2v).
-template <bool BNR>
+// BNR 1: ReLU mask and BN sums from the BN input x at every input pixel (as
+// maxpool_bwd_kernel); BNR 2: from the forward's per-window argmax input xsel
+// instead -- a pixel only receives gradient as some window's argmax, so its
+// mask and x are that window's (the same sums, term for term): x (4x the
+// pooled bytes) is not read.
+template <int BNR>
 __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy,
                                                                const uint8_t* __restrict__ idx,
                                                                bf16_t* __restrict__ dx, int N, int C, int OH,
@@ -305,8 +330,27 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
                 g[u * 2 + v] = ok ? *reinterpret_cast<const u32x4*>(dy + off) : u32x4{0u, 0u, 0u, 0u};
                 ii[u * 2 + v] = ok ? *reinterpret_cast<const u32x2*>(idx + off) : u32x2{0xffffffffu, 0xffffffffu};
             }
+        u32x4 xs[4];
+        if constexpr (BNR == 2) {  // each window's ReLU mask from its argmax input, applied to its gradient
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const bool ok = (int)i + u < OH && (int)j + v < OW;
+                    const size_t off = (((size_t)n * OH + i + (ok ? u : 0)) * OW + j + (ok ? v : 0)) * C + ch * 8;
+                    xs[u * 2 + v] = *reinterpret_cast<const u32x4*>(bnr.xsel + off);
+                    u32x4& gg = g[u * 2 + v];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        uint32_t gw = gg[c];
+                        if (!(fmaf(lo_bf(xs[u * 2 + v][c]), sc[2 * c], sh[2 * c]) > 0.f)) gw &= 0xffff0000u;
+                        if (!(fmaf(hi_bf(xs[u * 2 + v][c]), sc[2 * c + 1], sh[2 * c + 1]) > 0.f)) gw &= 0x0000ffffu;
+                        gg[c] = gw;
+                    }
+                }
+        }
         u32x4 xw[4];
-        if constexpr (BNR) {
+        if constexpr (BNR == 1) {
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -318,9 +362,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-                float acc[8];
+                float acc[8], xv[8];  // xv (BNR 2): the pixel's x, from a window that took it
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+                for (int c = 0; c < 8; ++c) acc[c] = xv[c] = 0.f;
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -333,11 +377,25 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
                         for (int c = 0; c < 4; ++c) {
                             const uint32_t w = c < 2 ? w2[0] : w2[1];
                             const int s8 = 16 * (c & 1);
-                            if ((int)((w >> s8) & 0xff) == want) acc[2 * c] += lo_bf(gg[c]);
-                            if ((int)((w >> (s8 + 8)) & 0xff) == want) acc[2 * c + 1] += hi_bf(gg[c]);
+                            if ((int)((w >> s8) & 0xff) == want) {
+                                acc[2 * c] += lo_bf(gg[c]);
+                                if constexpr (BNR == 2) xv[2 * c] = lo_bf(xs[u * 2 + v][c]);
+                            }
+                            if ((int)((w >> (s8 + 8)) & 0xff) == want) {
+                                acc[2 * c + 1] += hi_bf(gg[c]);
+                                if constexpr (BNR == 2) xv[2 * c + 1] = hi_bf(xs[u * 2 + v][c]);
+                            }
                         }
                     }
-                if constexpr (BNR) {
+                if constexpr (BNR == 2) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        const float gq = bf2f(f2bf(acc[c]));
+                        sg[c] += gq;
+                        sgx[c] += gq * ((xv[c] - mean[c]) * rstd[c]);
+                    }
+                }
+                if constexpr (BNR == 1) {
                     const u32x4 x4 = xw[a * 2 + b];
 #pragma unroll
                     for (int c = 0; c < 8; ++c) {
@@ -654,7 +712,7 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
     const long total = (long)N * H * W * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
     if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
-        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<false>), dim3(stream_grid(total / 4)), dim3(256), 0,
+        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<0>), dim3(stream_grid(total / 4)), dim3(256), 0,
                            (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
                            OW, PoolBnr{});
         IMK_CHECK_LAUNCH();
@@ -674,34 +732,42 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
 // BN(+ReLU) forward fused into the maxpool that consumes it (the stem): y =
 // maxpool(relu(bn(x))) with argmax indices; save <- (mean, rstd)
 IMK_EXPORT int imk_maxpool_fwd_bn(const void* x, const float* sums, const float* gamma, const float* beta,
-                                  float* save, void* y, void* idx, int N, int H, int W, int C, int OH, int OW,
-                                  int k, int s, int p, float eps, void* stream) {
+                                  float* save, void* y, void* idx, void* xsel, int N, int H, int W, int C, int OH,
+                                  int OW, int k, int s, int p, float eps, void* stream) {
     if (C % 8 || 256 % (C / 8) || k > 3) return -100;
     const long total = (long)N * OH * OW * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
     const dim3 g(stream_grid(total)), b(256);
     hipLaunchKernelGGL((maxpool_fwd_kernel<3, true>), g, b, 0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y,
                        (uint8_t*)idx, N, H, W, C, OH, OW, k, s, p,
-                       PoolBnf{sums, gamma, beta, save, 1.f / (float)((long)N * H * W), eps});
+                       PoolBnf{sums, gamma, beta, save, 1.f / (float)((long)N * H * W), eps, (bf16_t*)xsel});
     IMK_CHECK_LAUNCH();
     return 0;
 }
 
 // maxpool backward fused with the BN(+ReLU) backward reductions of the BN that
-// feeds the pool (the stem): dx = ReLU-masked gradient, slab += (sum g*xhat, sum g)
-IMK_EXPORT int imk_maxpool_bwd_bnr(const void* dy, const void* idx, void* dx, const void* x, const float* save,
-                                   const float* gamma, const float* beta, float* slab, int N, int H, int W,
-                                   int C, int OH, int OW, int k, int s, int p, void* stream) {
+// feeds the pool (the stem): dx = ReLU-masked gradient, slab += (sum g*xhat, sum g). xsel (the forward's
+// per-window argmax input, imk_maxpool_fwd_bn) replaces the read of x on the 2x2-quad path
+IMK_EXPORT int imk_maxpool_bwd_bnr(const void* dy, const void* idx, void* dx, const void* x, const void* xsel,
+                                   const float* save, const float* gamma, const float* beta, float* slab, int N,
+                                   int H, int W, int C, int OH, int OW, int k, int s, int p, void* stream) {
     if (C % 8 || C > 2048 || 256 % (C / 8) || (k + s - 1) / s > 2) return -100;
     const long total = (long)N * H * W * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
     if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
-        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<true>), dim3(stream_grid(total / 4)), dim3(256), 0,
-                           (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
-                           OW, PoolBnr{(const bf16_t*)x, save, gamma, beta, slab});
+        const PoolBnr bnr{(const bf16_t*)x, save, gamma, beta, slab, (const bf16_t*)xsel};
+        if (xsel)
+            hipLaunchKernelGGL((maxpool_bwd_quad_kernel<2>), dim3(stream_grid(total / 4)), dim3(256), 0,
+                               (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
+                               OW, bnr);
+        else
+            hipLaunchKernelGGL((maxpool_bwd_quad_kernel<1>), dim3(stream_grid(total / 4)), dim3(256), 0,
+                               (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
+                               OW, bnr);
         IMK_CHECK_LAUNCH();
         return 0;
     }
+    if (!x) return -100;  // the per-pixel path needs x
     const dim3 g(stream_grid(total)), b(256);
     hipLaunchKernelGGL((maxpool_bwd_kernel<2, true>), g, b, 0, (hipStream_t)stream, (const bf16_t*)dy,
                        (const uint8_t*)idx, (bf16_t*)dx, N, H, W, C, OH, OW, k, s, p,

@@ -175,9 +175,9 @@ def _declare(name: str, lib) -> None:
             "imk_bn_finalize_affine": [vp, vp, vp, vp, vp, vp, i32, i32, i64, f32, i32, vp],
             "imk_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
             "imk_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp],
-            "imk_maxpool_fwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+            "imk_maxpool_fwd_bn": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                    C.c_float, vp],
-            "imk_maxpool_bwd_bnr": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+            "imk_maxpool_bwd_bnr": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                     vp],
             "imk_avgpool_fwd": [vp, vp, i32, i32, i32, vp],
             "imk_avgpool_bwd": [vp, vp, i32, i32, i32, vp],

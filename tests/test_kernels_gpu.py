@@ -727,7 +727,7 @@ def test_maxpool_bwd_bn_reduce_fused(H):
     slab = torch.zeros(32, 3, C, device=DEV)
     g = torch.empty_like(x)
     _lib.check(_lib.kernels().imk_maxpool_bwd_bnr(dy.data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(),
-                                                  save.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                                  None, save.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                                                   slab.data_ptr(), N, H, H, C, OH, OH, 3, 2, 1,
                                                   _lib.stream_ptr()), "pool bwd bnr")
     assert rel(g, g_ref) < 1e-2
@@ -736,6 +736,58 @@ def test_maxpool_bwd_bn_reduce_fused(H):
     s = slab.sum(0)
     assert rel(s[0], (gb * xhat).sum((0, 1, 2))) < 1e-3
     assert rel(s[1], gb.sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("H", [30, 56])
+def test_maxpool_bnr_from_argmax_input(H):
+    """The stem pool's BN backward without re-reading x (StemFn): imk_maxpool_fwd_bn also stores the BN input at
+    each window's argmax (xsel); imk_maxpool_bwd_bnr given xsel takes every window's ReLU mask from it and sums
+    from the argmax input of a window that took each pixel -- the same gradient bit for bit as the x-reading pass,
+    and the same BN sums term for term."""
+    from imagent_amd.ops import _lib
+    from imagent_amd.ops.misc import MaxPoolFn
+    kern = _lib.kernels()
+    torch.manual_seed(8)
+    N, C, eps = 4, 64, 1e-5
+    x = bf(torch.randn(N, H, H, C, device=DEV))
+    mean, var = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    gamma, beta = torch.randn(C, device=DEV), torch.randn(C, device=DEV) * 0.3  # some gamma < 0
+    sums = torch.stack([mean, var]).contiguous()
+    OH = (H + 2 - 3) // 2 + 1
+    y = torch.empty(N, OH, OH, C, device=DEV, dtype=torch.bfloat16)
+    idx = torch.empty(y.shape, dtype=torch.uint8, device=DEV)
+    xsel = torch.empty_like(y)
+    save = torch.empty(2, C, device=DEV)
+    _lib.check(kern.imk_maxpool_fwd_bn(x.data_ptr(), sums.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                       save.data_ptr(), y.data_ptr(), idx.data_ptr(), xsel.data_ptr(), N, H, H, C,
+                                       OH, OH, 3, 2, 1, eps, _lib.stream_ptr()), "bn + pool")
+    sc = save[1] * gamma
+    sh = beta - save[0] * sc
+    h = torch.relu(x.float() * sc + sh).to(torch.bfloat16).requires_grad_(True)
+    yr = MaxPoolFn.apply(h, 3, 2, 1)
+    assert rel(y, yr) < 1e-3
+    # xsel holds an input of the window that maps to the pooled value
+    assert rel(torch.relu(xsel.float() * sc + sh), y.float()) < 1e-2
+    dy = bf(torch.randn_like(y.float()))
+    gs = []
+    for use_xsel in (False, True):
+        slab = torch.zeros(32, 3, C, device=DEV)
+        g = torch.empty_like(x)
+        _lib.check(kern.imk_maxpool_bwd_bnr(dy.data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(),
+                                            xsel.data_ptr() if use_xsel else None, save.data_ptr(),
+                                            gamma.data_ptr(), beta.data_ptr(), slab.data_ptr(), N, H, H, C, OH, OH,
+                                            3, 2, 1, _lib.stream_ptr()), "pool bwd bnr")
+        gs.append((g, slab.sum(0)))
+    (g1, s1), (g2, s2) = gs
+    assert torch.equal(g1, g2)
+    yr.backward(dy)
+    g_ref = h.grad.float() * (x.float() * sc + sh > 0)
+    assert rel(g2, g_ref) < 1e-2
+    gb = g2.float()
+    xhat = (x.float() - save[0]) * save[1]
+    assert rel(s2[0], (gb * xhat).sum((0, 1, 2))) < 1e-3
+    assert rel(s2[1], gb.sum((0, 1, 2))) < 1e-3
+    assert rel(s2[:2], s1[:2]) < 1e-5
 
 
 @pytest.mark.parametrize("R,Cc", [(512, 1000), (7, 10), (100, 64), (2048, 130)])
