@@ -142,10 +142,11 @@ class _NS:
         self.__dict__.update(kw)
 
 
-@pytest.mark.parametrize("p", [128, 256])
-def test_gram_statistics_large_mean(p):
+@pytest.mark.parametrize("p,sig", [(64, 0.2), (128, 0.3), (256, 0.3), (128, 0.1)])
+def test_gram_statistics_large_mean(p, sig):
     """bn3's statistics in the Gram form (ops/bn_gram.py gram_fwd_stats: x3 = h2 W3^T never formed) and on the
-    per-op path (conv epilogue, shifted sums) when |mean(x3)| / std(x3) >= 30: half of conv3's output channels
+    per-op path (conv epilogue, shifted sums) when |mean(x3)| / std(x3) >= 30 (>= 100 with sig = 0.1; |mean| / std ~
+    sqrt(p) / sig): half of conv3's output channels
     have weight rows aligned with the (positive, ReLU-like) mean of h2. Checked against fp64 statistics of
     h2 W3^T over the same bf16 operands: mean to 1e-3 sd, variance to 1e-3 relative. Also the x-free backward
     coefficient sum(g xhat3) (bn_bwd_coef_T_kernel: from T = g^T h2, centred per element) against fp64."""
@@ -156,14 +157,14 @@ def test_gram_statistics_large_mean(p):
     torch.manual_seed(7)
     N, H, C4 = 256, 32, 4 * p
     M = N * H * H
-    h2 = (1.0 + 0.3 * torch.randn(N, H, H, p, device=DEV)).clamp_min(0).to(torch.bfloat16)
+    h2 = (1.0 + sig * torch.randn(N, H, H, p, device=DEV)).clamp_min(0).to(torch.bfloat16)
     w = torch.randn(C4, p, device=DEV) / p ** 0.5
     w[: C4 // 2] = (1.0 + 0.1 * torch.randn(C4 // 2, p, device=DEV)) / p  # aligned rows: mean ~1, std ~0.3/sqrt(p)
     w3 = w.to(torch.bfloat16)
     x3 = h2.reshape(M, p).double() @ w3.double().t()
     mean64, var64 = x3.mean(0), x3.var(0, unbiased=False)
     sd64 = var64.sqrt()
-    assert float((mean64[: C4 // 2].abs() / sd64[: C4 // 2]).min()) >= 30.0
+    assert float((mean64[: C4 // 2].abs() / sd64[: C4 // 2]).min()) >= (100.0 if sig < 0.2 else 30.0)
     bn = _NS(work=_work(C4), weight=torch.rand(C4, device=DEV) + 0.5, bias=torch.randn(C4, device=DEV) * 0.1,
              eps=1e-5)
     conv = _NS(out_channels=C4, in_channels=p, w_bf16=w3.view(C4, 1, 1, p))
@@ -175,7 +176,7 @@ def test_gram_statistics_large_mean(p):
     mean, var = bn.work.stats[0].double(), bn.work.stats[1].double()
     e_mean = float(((mean - mean64).abs() / sd64).max())
     e_var = float(((var - var64).abs() / var64).max())
-    print(f"p={p}: Gram form mean err {e_mean:.2e} sd, var rel err {e_var:.2e}")
+    print(f"p={p} sig={sig}: Gram form mean err {e_mean:.2e} sd, var rel err {e_var:.2e}")
     assert e_mean < 1e-3 and e_var < 1e-3
     # per-op path: the conv epilogue's shifted sums over the stored bf16 x3 (second call: shift = first mean)
     work = _work(C4)
