@@ -159,10 +159,11 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
-    if (tile == 17 || tile == 18 || tile == 27 || tile == 28) {  // v3 main loop (conv_igemm_v3.h); 27 / 28: tap-inner
+    if (tile == 17 || tile == 18 || tile == 19 || tile == 27 || tile == 28) {  // v3 main loop (conv_igemm_v3.h); 19: 256x128; 27 / 28: tap-inner
         if (!use_lds || !v3_ok(a)) return -105;
         switch (tile) {
             case 17: return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+            case 19: return launch_v3<256, 128, 2, 2, 8, 128>(a, st);
             case 18: return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
             case 27: return launch_v3<256, 256, 2, 2, 8, 128, 2, 0, true>(a, st);
             default: return launch_v3<128, 128, 2, 2, 4, 128, 2, 0, true>(a, st);
@@ -187,6 +188,9 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
             }
             return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
         }
+        // (256x128 tiles on 8 waves for the 128-channel outputs, tile 19, round 5: forward 3-6 % faster stand-alone,
+        // dgrad 6 % and the fused BN-backward dgrads 7-21 % slower, in-step 16,822 / 16,842 vs 17,003 / 16,991 img/s
+        // -- not taken, profiles/r50_b2048_r5_v3_256x128.md)
         return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
     if (bnb || use_lds) {  // the tiles the auto choice makes, with a fused / staged epilogue

@@ -129,12 +129,12 @@ def test_conv_lds_epilogue(tile, shape):
     assert rel(acc.float() - base.float(), nhwc(xr.grad)) < 2e-2
 
 
-@pytest.mark.parametrize("tile", [17, 18])
+@pytest.mark.parametrize("tile", [17, 18, 19])
 @pytest.mark.parametrize("shape", [(4, 64, 14, 128, 3, 1, 1), (2, 256, 9, 512, 1, 1, 0), (2, 64, 8, 256, 1, 1, 0),
                                    (3, 128, 15, 320, 3, 1, 1), (3, 128, 15, 320, 3, 2, 1), (8, 256, 14, 256, 3, 1, 1),
                                    (2, 128, 9, 192, 1, 1, 0), (3, 64, 5, 192, 3, 2, 1), (2, 512, 7, 2048, 1, 1, 0)])
 def test_conv_v3(tile, shape):
-    """v3 main loop (conv_igemm_v3.h; 17: 256x256, 18: 128x128): buffer-descriptor LDS-DMA whose
+    """v3 main loop (conv_igemm_v3.h; 17: 256x256, 18: 128x128, 19: 256x128): buffer-descriptor LDS-DMA whose
     out-of-image taps / rows beyond M or Nout read the buffer unit's zeros -- padding borders,
     strided dgrad parity classes (taps with negative offsets), ragged M and N -- forward +
     statistics, dgrad, dgrad accumulate against fp32; 1 to 36 K-tiles."""
