@@ -245,6 +245,8 @@ def main(argv=None):
         t1 = time.perf_counter()
         coll_per_step = (comm.collectives - c0) / max(1, a.steps)
         T = max_over_ranks(t1 - t0)
+        # the mean loss of the warm-up + timed steps only (read before the instrumented steps below)
+        loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
         # after the timed region: two more steps with the bucket timeline recorded (parallel/ddp.py CommTimeline:
         # exposed communication after the last backward kernel, per-bucket issue offsets, comm-stream busy time)
         overlap = None
@@ -254,7 +256,6 @@ def main(argv=None):
             sync()
             overlap = ddp.timeline.stats()
             ddp.comm_timeline(False)
-        loss, _, _, _ = metrics.reduced(comm if ctx.world_size > 1 else None)
         n_rccl = rccl_communicators()  # counted while the training communicator is open
         val = None
         if a.eval > 0:  # validation throughput (Trainer.validate's step): eval-mode forward under no_grad
@@ -321,6 +322,8 @@ def main(argv=None):
                     "comm_nranks": getattr(comm, "nranks", comm.world_size),
                     "collectives_per_step": coll_per_step,
                     "comm_overlap": overlap,
+                    "comm_overlap_source": "2 instrumented steps after the timed region (not the timed steps)"
+                    if overlap is not None else None,
                     "wgrad_side_stream": bool(a.wgrad_overlap) and a.kernels == "hip" and not f32_hip,
                     "auto_batch_reduced": auto_reduced,
                     "bucket_mb": a.bucket_mb,

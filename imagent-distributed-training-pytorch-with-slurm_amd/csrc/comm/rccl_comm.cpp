@@ -309,7 +309,11 @@ int32_t imc_comm_destroy(void* h) {
     if (!c) return 0;
     int expect = 0;
     if (c->owner.compare_exchange_strong(expect, 2, std::memory_order_seq_cst)) {
-        if (c->stream && !c->aborting.load(std::memory_order_seq_cst)) (void)hipStreamSynchronize(c->stream);
+        // drain the comm stream by polling, not a blocking sync: a collective hung on a dead peer never finishes,
+        // and the watchdog's imc_abort (which lost the ownership race to this destroy) only raises `aborting` --
+        // seeing it, this thread stops waiting and calls ncclCommAbort itself, which unblocks the stream
+        while (c->stream && !c->aborting.load(std::memory_order_seq_cst) && hipStreamQuery(c->stream) == hipErrorNotReady)
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
         if (c->comm) {
             // a non-blocking communicator finalises asynchronously; settle() leaves early once a concurrent
             // imc_abort raised `aborting` (that abort lost the ownership race and does not touch the handle)

@@ -30,6 +30,14 @@ import torch.nn.functional as F
 # below 100 % top-1 within a short run, so a numerics regression shows as a lower curve
 MIX_SIGMA = 1.4
 MIX_DIM = 32
+MIX_CHUNK_BYTES = 1 << 30  # host fp32 working set of one render chunk
+
+
+def mix_pool_cap(batch_size: int, image_size: int, budget_gb: Optional[float] = None) -> int:
+    """Most batches a resident task='mix' pool may hold: IMAGENT_MIX_POOL_GB (default 16) of uint8 images."""
+    import os
+    gb = float(os.environ.get("IMAGENT_MIX_POOL_GB", "16")) if budget_gb is None else budget_gb
+    return max(1, int(gb * (1 << 30)) // (batch_size * image_size * image_size * 3))
 
 
 def _mix_model(num_classes: int, image_size: int):
@@ -106,8 +114,15 @@ class SyntheticImageNet:
             self.labels = self.labels.to(self.device)
         elif task == "mix":
             self.labels = torch.randint(0, num_classes, (pb, batch_size), generator=g)
-            img = mix_render(self.labels.view(-1), image_size, num_classes, g, sigma=mix_sigma)
-            self.images = img.view(pb, batch_size, image_size, image_size, 3).to(self.device)
+            # rendered in chunks of whole batches (mix_render's fp32 intermediate is 4x the uint8 images) straight
+            # into the resident device pool
+            self.images = torch.empty((pb, batch_size, image_size, image_size, 3), dtype=torch.uint8,
+                                      device=self.device)
+            per = max(1, MIX_CHUNK_BYTES // (4 * batch_size * image_size * image_size * 3))
+            for b0 in range(0, pb, per):
+                b1 = min(pb, b0 + per)
+                img = mix_render(self.labels[b0:b1].reshape(-1), image_size, num_classes, g, sigma=mix_sigma)
+                self.images[b0:b1].copy_(img.view(b1 - b0, batch_size, image_size, image_size, 3))
             self.labels = self.labels.to(self.device)
         else:
             raise ValueError(f"unknown synthetic task {task!r}")

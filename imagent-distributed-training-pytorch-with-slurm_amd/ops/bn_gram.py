@@ -170,6 +170,8 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
     when they are formed here (the per-step workspace), else fresh zeroed tensors.
     Returns the side-stream event after the last read of ``g`` (or None without a side stream):
     the caller's next writer of ``g`` (conv1's accumulating dgrad) waits for it."""
+    if bn is None:  # its saved batch mean enters the fix-up, and the side stream protects its workspace
+        raise ValueError("gram_wgrad needs bn (the block's bn3)")
     side = streams.side_stream(h2.device) if h2.is_cuda else None
     if side is not None:
         side.wait_stream(torch.cuda.current_stream(h2.device))

@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from ..data.loader import DeviceLoader, InputTransform, SyntheticLoader
-from ..data.synthetic import SyntheticImageNet
+from ..data.synthetic import SyntheticImageNet, mix_pool_cap
 from ..models import resnet
 from ..models.arena import ParamArena
 from ..parallel import launcher
@@ -234,15 +234,19 @@ class Trainer:
             task = getattr(a, "synthetic_task", "random")
             # mix: every training batch distinct (the accuracy must come from generalising, not recall)
             pool = 4 if task == "random" else 16 if task == "colour" else None
+            vpool = pool
             if pool is None:
-                pool = max(1, min(a.synthetic_train_size // a.batch_size, 4096))
+                # capped by bytes (the pool is rendered once and stays resident in HBM): at most
+                # IMAGENT_MIX_POOL_GB (default 16) per pool, train and validation alike
+                cap = mix_pool_cap(a.batch_size, a.image_size)
+                pool = max(1, min(a.synthetic_train_size // a.batch_size, cap))
+                vpool = max(1, min(a.synthetic_val_size // a.batch_size, cap))
             self.train_src = SyntheticImageNet(a.synthetic_train_size, a.image_size, a.num_classes,
                                                a.batch_size, self.device, a.seed, rank=rk, task=task,
                                                pool_batches=pool)
             self.val_src = SyntheticImageNet(a.synthetic_val_size, a.image_size, a.num_classes,
                                              a.batch_size, self.device, a.seed + 1, rank=rk, task=task,
-                                             pool_batches=pool if task != "mix" else
-                                             max(1, a.synthetic_val_size // a.batch_size))
+                                             pool_batches=vpool)
             self.n_train, self.n_val = a.synthetic_train_size, a.synthetic_val_size
             self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=a.seed)
             self.val_sampler = ShardSampler(self.n_val, ws, rk, shuffle=True, seed=a.seed)

@@ -77,3 +77,18 @@ def test_collate():
     imgs, labels = collate_u8([(torch.zeros(2, 2, 3, dtype=torch.uint8), 1),
                                (torch.ones(2, 2, 3, dtype=torch.uint8), 4)])
     assert imgs.shape == (2, 2, 2, 3) and labels.tolist() == [1, 4]
+
+
+def test_mix_pool_is_byte_capped_and_chunked(monkeypatch):
+    """task='mix' renders its resident pool in chunks of whole batches, and the trainer caps the pool by bytes
+    (the CLI defaults asked for ~316 GB of images)."""
+    from imagent_amd.data import synthetic as S
+    assert S.mix_pool_cap(128, 448, budget_gb=16) == (16 << 30) // (128 * 448 * 448 * 3)
+    assert S.mix_pool_cap(128, 448, budget_gb=1e-9) == 1
+    whole = SyntheticImageNet(5 * 8, 16, 10, 8, "cpu", seed=3, pool_batches=5, task="mix")
+    monkeypatch.setattr(S, "MIX_CHUNK_BYTES", 4 * 8 * 16 * 16 * 3 * 2)  # 2 batches per chunk
+    chunked = SyntheticImageNet(5 * 8, 16, 10, 8, "cpu", seed=3, pool_batches=5, task="mix")
+    assert chunked.images.shape == (5, 8, 16, 16, 3) and chunked.images.dtype == torch.uint8
+    assert torch.equal(whole.labels, chunked.labels)
+    # same class -> appearance map and value range, a different per-chunk noise draw
+    assert abs(whole.images.float().mean().item() - chunked.images.float().mean().item()) < 4.0
