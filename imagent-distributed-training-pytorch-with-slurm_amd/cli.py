@@ -53,6 +53,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="random: uniform noise + labels (throughput); colour: learnable class-coloured images; "
                         "mix: overlapping class Gaussians over smooth random bases (Bayes top-1 ~85 %% at 100 classes)")
     p.add_argument("--flip", action="store_true", help="random horizontal flip (reference: none)")
+    p.add_argument("--record-resize", action="store_true",
+                   help="records stored at another size than --image-size are bilinearly resampled on the GPU "
+                        "(fused into the normalise kernel) instead of cropped: e.g. 320^2 records for 448^2 "
+                        "training halve the host gather bytes (profiles/loader_throughput.md)")
     # --- optimisation ---
     p.add_argument("--optimizer", default="sgd",
                    choices=["sgd", "lars", "adam", "adamw", "adagrad", "rmsprop", "adadelta", "asgd", "nadam"])

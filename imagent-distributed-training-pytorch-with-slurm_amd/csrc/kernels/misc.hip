@@ -647,6 +647,55 @@ __global__ __launch_bounds__(256) void normalize_kernel(const uint8_t* __restric
     }
 }
 
+// --------------------------------------------------------- resize + normalize (uint8)
+// The record store at a smaller size than the model input (data/records.py, --record-resize): in uint8
+// [B][Hs][Ws][3] -> out bf16 [B][H][W][Cp] with a bilinear resample (half-pixel centres, edge clamp:
+// torch's interpolate(bilinear, align_corners=False) and PIL's upscaling filter) fused into the normalize,
+// optional horizontal flip. One thread per output pixel; its 4 source pixels are 12 bytes of 2 rows, served
+// by L2 (each source pixel is read by ~(H/Hs)^2 neighbouring threads).
+__global__ __launch_bounds__(256) void resize_normalize_kernel(const uint8_t* __restrict__ in,
+                                                               bf16_t* __restrict__ out,
+                                                               const uint8_t* __restrict__ flip, int B, int Hs,
+                                                               int Ws, int H, int W, int Cp, float m0, float m1,
+                                                               float m2, float is0, float is1, float is2) {
+    const long total = (long)B * H * W;
+    const float sy = (float)Hs / (float)H, sx = (float)Ws / (float)W;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const int w = t % W;
+        const long r = t / W;
+        const int h = r % H;
+        const int b = r / H;
+        const int ww = (flip && flip[b]) ? (W - 1 - w) : w;
+        const float fy = fmaxf((h + 0.5f) * sy - 0.5f, 0.f), fx = fmaxf((ww + 0.5f) * sx - 0.5f, 0.f);
+        const int y0 = min((int)fy, Hs - 1), x0 = min((int)fx, Ws - 1);
+        const int y1 = min(y0 + 1, Hs - 1), x1 = min(x0 + 1, Ws - 1);
+        const float ly = fy - (float)y0, lx = fx - (float)x0;
+        const uint8_t* row0 = in + ((size_t)b * Hs + y0) * Ws * 3;
+        const uint8_t* row1 = in + ((size_t)b * Hs + y1) * Ws * 3;
+        float c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float top = (float)row0[x0 * 3 + k] * (1.f - lx) + (float)row0[x1 * 3 + k] * lx;
+            const float bot = (float)row1[x0 * 3 + k] * (1.f - lx) + (float)row1[x1 * 3 + k] * lx;
+            c[k] = top * (1.f - ly) + bot * ly;
+        }
+        const float c0 = (c[0] * (1.f / 255.f) - m0) * is0;
+        const float c1 = (c[1] * (1.f / 255.f) - m1) * is1;
+        const float c2 = (c[2] * (1.f / 255.f) - m2) * is2;
+        bf16_t* o = out + (size_t)t * Cp;
+        if (Cp == 8) {
+            *reinterpret_cast<u32x4*>(o) = u32x4{pack_bf2(c0, c1), pack_bf2(c2, 0.f), 0u, 0u};
+        } else if (Cp == 4) {
+            *reinterpret_cast<u32x2*>(o) = u32x2{pack_bf2(c0, c1), pack_bf2(c2, 0.f)};
+        } else {
+            o[0] = f2bf(c0);
+            o[1] = f2bf(c1);
+            o[2] = f2bf(c2);
+            for (int cc = 3; cc < Cp; ++cc) o[cc] = 0;
+        }
+    }
+}
+
 // ------------------------------------------------- batched weight transposes
 // dst[ci][t][co] = src[co][t][ci]  for every conv in the descriptor table.
 struct TDesc {
@@ -889,6 +938,16 @@ IMK_EXPORT int imk_cast_bf16(const float* p, void* o, long n, void* stream) {
 IMK_EXPORT int imk_uncast_bf16(const void* i, float* o, long n, void* stream) {
     hipLaunchKernelGGL(uncast_bf16_kernel, dim3(stream_grid(n)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)i, o, n);
+    IMK_CHECK_LAUNCH();
+    return 0;
+}
+
+IMK_EXPORT int imk_resize_normalize_u8(const void* in, void* out, const void* flip, int B, int Hs, int Ws, int H,
+                                       int W, int Cp, const float* mean, const float* std, void* stream) {
+    if (Hs < 1 || Ws < 1 || H < 1 || W < 1 || Cp < 3) return -1;
+    hipLaunchKernelGGL(resize_normalize_kernel, dim3(stream_grid((long)B * H * W)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint8_t*)in, (bf16_t*)out, (const uint8_t*)flip, B, Hs, Ws, H,
+                       W, Cp, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2]);
     IMK_CHECK_LAUNCH();
     return 0;
 }

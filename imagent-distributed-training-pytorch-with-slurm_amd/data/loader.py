@@ -33,11 +33,14 @@ class InputTransform:
     """uint8 [B,H,W,3] (on the compute device) -> model input."""
 
     def __init__(self, backend: str, size: Tuple[int, int], mean=MEAN, std=STD, cpad: int = 8,
-                 flip: bool = False, dtype=torch.float32):
+                 flip: bool = False, dtype=torch.float32, resize: bool = False):
         self.backend, self.size = backend, tuple(size)
         self.mean, self.std, self.cpad = tuple(mean), tuple(std), cpad
         self.flip = flip
         self.dtype = dtype
+        # resize: an image of another size is bilinearly resampled to `size` (records stored smaller than the
+        # model input, --record-resize) instead of randomly cropped
+        self.resize = resize
 
     def __call__(self, u8: torch.Tensor) -> torch.Tensor:
         B, H, W, _ = u8.shape
@@ -49,12 +52,21 @@ class InputTransform:
             crop = flip = None
             if self.flip:
                 flip = torch.randint(0, 2, (B,), dtype=torch.uint8, device=u8.device)
+            if self.resize and (H, W) != (oh, ow):
+                if self.backend == "hip_f32":
+                    raise NotImplementedError("--record-resize: the bf16 input path only")
+                from ..ops.misc import resize_normalize_u8
+                return resize_normalize_u8(u8, (oh, ow), self.cpad, self.mean, self.std, flip)
             if (H, W) != (oh, ow):
                 cy = torch.randint(0, H - oh + 1, (B,), dtype=torch.int32, device=u8.device)
                 cx = torch.randint(0, W - ow + 1, (B,), dtype=torch.int32, device=u8.device)
                 crop = torch.stack([cy, cx], 1).contiguous()
             return normalize_u8(u8, (oh, ow), self.cpad, self.mean, self.std, crop, flip)
-        x = u8[:, :oh, :ow].permute(0, 3, 1, 2).to(self.dtype).div_(255.0)
+        if self.resize and (H, W) != (oh, ow):
+            x = torch.nn.functional.interpolate(u8.permute(0, 3, 1, 2).float(), size=(oh, ow), mode="bilinear",
+                                                align_corners=False).to(self.dtype).div_(255.0)
+        else:
+            x = u8[:, :oh, :ow].permute(0, 3, 1, 2).to(self.dtype).div_(255.0)
         m = torch.tensor(self.mean, dtype=self.dtype, device=u8.device).view(1, 3, 1, 1)
         s = torch.tensor(self.std, dtype=self.dtype, device=u8.device).view(1, 3, 1, 1)
         x = (x - m) / s

@@ -277,6 +277,24 @@ class TransposePlan:
 
 
 # -------------------------------------------------------------- normalize
+def resize_normalize_u8(images: torch.Tensor, out_hw, cpad: int, mean: Sequence[float], std: Sequence[float],
+                        flip: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [B, Hs, Ws, 3] -> bf16 NHWC [B, H, W, cpad]: bilinear resample to (H, W) (half-pixel centres,
+    ``F.interpolate(mode='bilinear', align_corners=False)``) fused with (x/255 - mean)/std -- the records stored
+    smaller than the model input (``--record-resize``), resized on the GPU instead of on the host
+    (imagenet.py:281's Resize, moved after the gather)."""
+    B, Hs, Ws, _ = images.shape
+    H, W = out_hw
+    if out is None:
+        out = torch.empty((B, H, W, cpad), device=images.device, dtype=torch.bfloat16)
+    m = (C.c_float * 3)(*mean)
+    s = (C.c_float * 3)(*std)
+    _lib.check(_lib.kernels().imk_resize_normalize_u8(images.data_ptr(), out.data_ptr(), _lib.ptr(flip), B, Hs, Ws,
+                                                      H, W, cpad, C.cast(m, C.c_void_p), C.cast(s, C.c_void_p),
+                                                      _lib.stream_ptr()), "resize + normalize")
+    return out
+
+
 def normalize_u8(images: torch.Tensor, out_hw, cpad: int, mean: Sequence[float], std: Sequence[float],
                  crop: Optional[torch.Tensor] = None, flip: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -61,6 +61,8 @@ class StepRunner:
         # on the step `max_inflight` back keeps the GPU fed and the footprint bounded.
         self.max_inflight = int(os.environ.get("IMAGENT_MAX_INFLIGHT", "2"))
         self._blocking = os.environ.get("IMAGENT_THROTTLE", "block") == "block"
+        # IMAGENT_STEP_SYNC=1 (diagnostics): device-synchronise after every step -- no run-ahead at all
+        self._step_sync = os.environ.get("IMAGENT_STEP_SYNC", "0") == "1"
         self._inflight: collections.deque = collections.deque()
 
     def _throttle(self, dev: torch.device) -> None:
@@ -117,6 +119,8 @@ class StepRunner:
         if streams.deferred():  # a deferred weight gradient nobody issued: a graph without a flush point
             raise RuntimeError("weight-gradient launches left queued after backward")
         self.opt.step()
+        if self._step_sync and micro[0][0].is_cuda:
+            torch.cuda.synchronize()
         self._throttle(micro[0][0].device)
 
     @torch.no_grad()
@@ -256,8 +260,9 @@ class Trainer:
             self.train_set = RecordFile(os.path.join(root, "train.imrec"), threads=a.workers)
             self.val_set = RecordFile(os.path.join(root, "val.imrec"), threads=a.workers)
             H, W, _ = self.train_set.shape
-            if H < size[0] or W < size[1]:
-                raise SystemExit(f"records hold {H}x{W} images, smaller than --image-size {a.image_size}")
+            if (H < size[0] or W < size[1]) and not getattr(a, "record_resize", False):
+                raise SystemExit(f"records hold {H}x{W} images, smaller than --image-size {a.image_size} "
+                                 "(--record-resize: resample them on the GPU)")
             self.num_classes = self.train_set.num_classes
             self.n_train, self.n_val = len(self.train_set), len(self.val_set)
             self.train_sampler = ShardSampler(self.n_train, ws, rk, shuffle=True, seed=0)
@@ -278,11 +283,11 @@ class Trainer:
         self.dtype = {"bf16": torch.bfloat16, "fp8": torch.bfloat16, "fp32": torch.float32}[a.dtype]
         if a.dtype == "fp8" and self.kernels != "hip":
             raise SystemExit("--dtype fp8 needs the HIP kernels (--kernels hip on a MI355X)")
+        rs = getattr(a, "record_resize", False)
         self.transform_train = InputTransform(self.kernels, size, cpad=resnet.ResNet.STEM_CPAD,
-                                              flip=a.flip,
-                                              dtype=torch.float32)
+                                              flip=a.flip, dtype=torch.float32, resize=rs)
         self.transform_val = InputTransform(self.kernels, size, cpad=resnet.ResNet.STEM_CPAD,
-                                            dtype=torch.float32)
+                                            dtype=torch.float32, resize=rs)
 
     def _loaders(self, epoch: int):
         a = self.args

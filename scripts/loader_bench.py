@@ -67,13 +67,13 @@ def gather_rate(path, ranks, threads, batch, iters):
     return sum(done) / dt
 
 
-def loader_rate(path, threads, batch, iters):
+def loader_rate(path, threads, batch, iters, out_size=None):
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.data.records import RecordFile, RecordLoader
     from imagent_amd.parallel.sampler import ShardSampler
     rf = RecordFile(path, threads=threads)
-    size = rf.shape[0]
-    tf = InputTransform("hip", (size, size), cpad=4)
+    size = out_size or rf.shape[0]
+    tf = InputTransform("hip", (size, size), cpad=4, resize=size != rf.shape[0])
     dl = RecordLoader(rf, ShardSampler(len(rf), 1, 0, shuffle=True, seed=0), batch, tf, "cuda:0")
     seen, t0 = 0, None
     for it in range(iters + 2):
@@ -113,17 +113,19 @@ def main():
     a = ap.parse_args()
     rows = []
     d = a.dir or tempfile.mkdtemp(prefix="imrec_")
-    for size in [int(s) for s in a.sizes.split(",")]:
+    # "448@320": 448^2 model input from records stored at 320^2 (GPU resample, --record-resize)
+    for spec in a.sizes.split(","):
+        size, stored = (int(v) for v in spec.split("@")) if "@" in spec else (int(spec), int(spec))
         n = 4096 if size >= 448 else 8192
-        path = os.path.join(d, f"bench_{size}.imrec")
+        path = os.path.join(d, f"bench_{stored}.imrec")
         if not os.path.exists(path):
-            make_records(path, n, size)
+            make_records(path, n, stored)
         g1 = gather_rate(path, 1, a.threads, a.batch, a.iters)
         gn = gather_rate(path, a.ranks, a.threads, a.batch, a.iters)
-        lr = loader_rate(path, a.threads, a.batch, 2) if torch.cuda.is_available() else float("nan")
+        lr = loader_rate(path, a.threads, a.batch, 2, size) if torch.cuda.is_available() else float("nan")
         pr = pil_rate(size)
-        rows.append((size, g1, gn, lr, pr))
-        print(f"{size}x{size}: gather 1 rank {g1:,.0f} img/s, {a.ranks} ranks {gn:,.0f} img/s; "
+        rows.append((spec.replace("@", "² from "), g1, gn, lr, pr))
+        print(f"{spec}: gather 1 rank {g1:,.0f} img/s, {a.ranks} ranks {gn:,.0f} img/s; "
               f"RecordLoader+H2D+normalise (1 rank) {lr:,.0f} img/s; PIL decode+resize {pr:,.0f} img/s/core",
               flush=True)
         os.remove(path)

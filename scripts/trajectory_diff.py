@@ -48,8 +48,9 @@ def rel(a: torch.Tensor, b: torch.Tensor) -> float:
 
 
 class Tracer:
-    def __init__(self, tr: Trainer, out, every: int = 1, eval_check: bool = True):
+    def __init__(self, tr: Trainer, out, every: int = 1, eval_check: bool = True, lockstep: bool = False):
         self.tr, self.out, self.every = tr, out, max(1, every)
+        self.lockstep = lockstep
         self.model = tr.model
         dev = tr.device
         self.ref = resnet.build(tr.args.arch, num_classes=tr.num_classes).to(dev)
@@ -81,10 +82,28 @@ class Tracer:
 
         def step():
             torch.cuda.synchronize()
-            self._G = self.tr.arena.G.clone()
+            ar = self.tr.arena
+            self._G = ar.G.clone()
+            self._P = ar.P.clone()
+            self._buf = opt.buf.clone() if getattr(opt, "buf", None) is not None else None
             opt.step = orig
             orig()
         opt.step = step
+
+    def _check_update(self, rec):
+        """The SGD step the HIP kernel took vs torch.optim.SGD's math from the same (P, G, momentum) (the
+        reference's optimizer, imagenet.py:325), and the bf16 compute shadows vs the new masters."""
+        opt, ar = self.tr.opt, self.tr.arena
+        g = opt.param_groups[0]
+        lr, mu, wd = g["lr"], g["momentum"], g["weight_decay"]
+        d = self._G + wd * self._P
+        if mu != 0:
+            buf = d if self._buf is None else self._buf * mu + d
+            d = buf
+        want = self._P - lr * d
+        rec["sgd_step_err"] = rel(ar.P - self._P, want - self._P)
+        if ar.S is not None:
+            rec["shadow_err"] = rel(ar.S.float(), ar.P.to(torch.bfloat16).float())
 
     def _ref_grads(self, sd, x, y, autocast: bool):
         ref = self.ref
@@ -101,7 +120,42 @@ class Tracer:
                 for n, m in ref.named_modules() if isinstance(m, resnet.BatchNorm2d)}
         return loss.item(), grads, bufs, logits.detach().float()
 
+    # ---- lockstep: PyTorch fp32 and bf16-autocast trainers on their OWN trajectories from the same start
+    def _lockstep_init(self):
+        dev = self.tr.device
+        sd = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        g = self.tr.opt.param_groups[0]
+        self.lock = {}
+        for name in ("fp32", "bf16"):
+            m = resnet.build(self.tr.args.arch, num_classes=self.tr.num_classes).to(dev)
+            m.load_state_dict(sd)
+            o = torch.optim.SGD(m.parameters(), lr=g["lr"], momentum=g["momentum"], weight_decay=g["weight_decay"])
+            self.lock[name] = (m, o)
+
+    def _lockstep_step(self, x, y, lr, rec):
+        xt = to_nchw(x)
+        flat = {}
+        for name, (m, o) in self.lock.items():
+            m.train()
+            o.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=name == "bf16"):
+                logits = m.forward_torch(xt)
+            loss = F.cross_entropy(logits.float(), y)
+            loss.backward()
+            for pg in o.param_groups:
+                pg["lr"] = lr
+            o.step()
+            rec[f"lock_loss_{name}"] = loss.item()
+            flat[name] = torch.cat([p.detach().reshape(-1) for _, p in sorted(m.named_parameters())])
+        hip = torch.cat([p.detach().reshape(-1) for _, p in sorted(self.model.named_parameters())])
+        n32 = flat["fp32"].norm().item()
+        rec["dist_hip_fp32"] = (hip - flat["fp32"]).norm().item() / n32
+        rec["dist_bf16_fp32"] = (flat["bf16"] - flat["fp32"]).norm().item() / n32
+        rec["dist_hip_bf16"] = (hip - flat["bf16"]).norm().item() / n32
+
     def train_step(self, micro):
+        if self.lockstep and not hasattr(self, "lock"):
+            self._lockstep_init()
         trace = self.step % self.every == 0 and len(micro) == 1
         if not trace:
             self._orig_train_step(micro)
@@ -120,6 +174,10 @@ class Tracer:
         lh = self._loss.item()
         rec = dict(step=self.step, lr=self.tr.opt.param_groups[0]["lr"], loss_hip=lh, loss_fp32=l32,
                    loss_bf16=l16)
+        if hasattr(self.tr.opt, "buf"):
+            self._check_update(rec)
+        if self.lockstep:
+            self._lockstep_step(x, y, rec["lr"], rec)
         eh, eb = {}, {}
         for n in self.names:
             eh[n] = rel(gh[n], g32[n])
@@ -153,10 +211,15 @@ class Tracer:
             rec["per_layer_bf16"] = {n: round(eb[n], 5) for n in self.names}
         self.out.write(json.dumps(rec) + "\n")
         self.out.flush()
+        if self.lockstep and self.step % 10 == 0:
+            print(f"[lock] step {self.step} loss hip {lh:.4f} fp32 {rec['lock_loss_fp32']:.4f} bf16 "
+                  f"{rec['lock_loss_bf16']:.4f} | |P_hip - P_fp32| {rec['dist_hip_fp32']:.3e} |P_bf16 - P_fp32| "
+                  f"{rec['dist_bf16_fp32']:.3e} |P_hip - P_bf16| {rec['dist_hip_bf16']:.3e}", flush=True)
         if self.step % 10 == 0:
             print(f"[traj] step {self.step} lr {rec['lr']:.4g} loss hip {lh:.4f} fp32 {l32:.4f} bf16 {l16:.4f} | "
                   f"gerr hip {rec['gerr_hip']:.4f} bf16 {rec['gerr_bf16']:.4f} | worst {worst} "
-                  f"{eh[worst]:.4f}/{eb[worst]:.4f} | bn var {rv:.2e}/{rv16:.2e}", flush=True)
+                  f"{eh[worst]:.4f}/{eb[worst]:.4f} | bn var {rv:.2e}/{rv16:.2e} | sgd {rec.get('sgd_step_err', -1):.1e} "
+                  f"shadow {rec.get('shadow_err', -1):.1e}", flush=True)
         self.step += 1
 
     @torch.no_grad()
@@ -176,6 +239,16 @@ class Tracer:
             n += y.numel()
         rec = dict(validate=True, after_step=self.step, hip_val_loss=res[0], hip_val_top1=res[1],
                    torch_eval_val_loss=tot / n, torch_eval_val_top1=100.0 * hits / n)
+        for name, (m, _) in getattr(self, "lock", {}).items():
+            m.eval()
+            lt = nt = 0.0
+            for x, y in val_loader:
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=name == "bf16"):
+                    lg = m.forward_torch(to_nchw(x)).float()
+                lt += F.cross_entropy(lg, y, reduction="sum").item()
+                nt += y.numel()
+            rec[f"lock_{name}_val_loss"] = lt / nt
+            print(f"[lock] validate after step {self.step}: {name} trajectory val loss {lt / nt:.4f}", flush=True)
         self.out.write(json.dumps(rec) + "\n")
         self.out.flush()
         print(f"[traj] validate after step {self.step}: HIP eval loss {res[0]:.4f} top1 {res[1]:.2f} | torch eval "
@@ -188,6 +261,9 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--out", required=True)
     ap.add_argument("--every", type=int, default=1, help="trace every N-th step")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="also train PyTorch fp32 and bf16-autocast models on their own trajectories from the same "
+                         "start (same batches, lr, SGD) and log the parameter distances between the three")
     ap.add_argument("rest", nargs=argparse.REMAINDER, help="-- then trainer CLI flags")
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
@@ -197,7 +273,7 @@ def main():
     with open(a.out, "w") as f:
         f.write(json.dumps(dict(config=vars(args))) + "\n")
         tr = Trainer(args)
-        Tracer(tr, f, every=a.every)
+        Tracer(tr, f, every=a.every, lockstep=a.lockstep)
         try:
             tr.run()
         finally:

@@ -92,3 +92,13 @@ def test_mix_pool_is_byte_capped_and_chunked(monkeypatch):
     assert torch.equal(whole.labels, chunked.labels)
     # same class -> appearance map and value range, a different per-chunk noise draw
     assert abs(whole.images.float().mean().item() - chunked.images.float().mean().item()) < 4.0
+
+
+def test_cpu_transform_resize_is_interpolate():
+    """--record-resize on the torch path: bilinear (align_corners=False) then ToTensor/Normalize."""
+    import torch.nn.functional as F
+    u8 = torch.randint(0, 256, (2, 20, 30, 3), dtype=torch.uint8)
+    x = InputTransform("torch", (40, 24), resize=True)(u8)
+    ref = F.interpolate(u8.permute(0, 3, 1, 2).float(), size=(40, 24), mode="bilinear", align_corners=False)
+    assert x.shape == (2, 3, 40, 24)
+    assert torch.allclose(x, (ref / 255.0 - 0.5) / 0.5, atol=1e-5)

@@ -105,3 +105,63 @@ def test_r50_forward_4096_duplicated():
         l2 = m(normalize_u8(torch.cat([img, img]), (224, 224), 4, mean, std)).float()
     assert torch.isfinite(l2).all()
     assert rel(l2[:2048], l1) < 2e-2 and rel(l2[2048:], l1) < 2e-2, (rel(l2[:2048], l1), rel(l2[2048:], l1))
+
+
+def test_train_step_4096_duplicated_halves():
+    """A TRAINING step (forward with batch statistics + backward) at 4096 img on a duplicated 2048-image batch, on a
+    bottleneck net with the whole stem and layer 1 (blocks [3, 1, 1, 1]): the stem output and the 256-channel layer-1
+    tensors hold 3.3 G elements (6.6 GB: past 2^31 elements and past the 32-bit byte range of one buffer descriptor).
+    With both halves identical, every per-pixel kernel sees identical per-channel constants (BatchNorm statistics and
+    backward reductions are over the whole batch), so the logits and the gradient flowing into EVERY block input must
+    be the same in both halves, bit for bit: any 32-bit element / byte index that wraps shows up as a mismatch. The
+    weight gradients (reductions) must equal the 2048-image step's up to summation order: compared with the
+    2048-vs-2048 rerun (the float-atomic noise floor)."""
+    from imagent_amd.models import resnet
+    from imagent_amd.models.native import bind_native
+    from imagent_amd.ops import block as blk
+    from imagent_amd.ops.misc import XentFn, normalize_u8
+    dev = torch.device(DEV)
+    torch.manual_seed(0)
+    m = resnet.ResNet(resnet.Bottleneck, [3, 1, 1, 1])
+    st = bind_native(m, dev)
+    m.train()
+    B = 2048
+    img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, 1000, (B,), device=dev)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    halves = []
+    orig = blk.BlockFn.apply
+
+    def apply(y, b):
+        if y.requires_grad and y.shape[0] == 2 * B:
+            y.register_hook(lambda g, n=len(halves): halves.append((n, tuple(g.shape), int((g[:B] != g[B:]).sum()))))
+        return orig(y, b)
+
+    def step(images, labels):
+        st.arena.G.zero_()
+        met = torch.zeros(4, device=dev)
+        logits = m(normalize_u8(images, (224, 224), 4, mean, std))
+        loss = XentFn.apply(logits, labels, met, 0.0)
+        loss.backward()
+        torch.cuda.synchronize()
+        return logits.detach(), st.arena.G.clone()
+
+    _, g1 = step(img, lab)
+    _, g1b = step(img, lab)
+    blk.BlockFn.apply = apply
+    try:
+        logits2, g2 = step(torch.cat([img, img]), torch.cat([lab, lab]))
+    finally:
+        del blk.BlockFn.apply  # back to the inherited torch.autograd.Function.apply
+    assert torch.isfinite(logits2).all()
+    assert torch.equal(logits2[:B], logits2[B:]), "forward: the two halves differ"
+    assert len(halves) == 6, halves
+    assert all(bad == 0 for _, _, bad in halves), halves
+    # weight gradients: the duplicated step vs the 2048 step, against the 2048-vs-2048 noise floor, per tensor
+    ar = st.arena
+    worst = 0.0
+    for i, name in enumerate(ar.names):
+        a, b, c = ar.flat_slice(g2, i), ar.flat_slice(g1, i), ar.flat_slice(g1b, i)
+        floor = rel(c, b)
+        worst = max(worst, rel(a, b) / max(floor, 1e-4))
+    assert worst < 10.0, worst
