@@ -1,25 +1,30 @@
-"""End-to-end training runs of the CLI on the HIP path (imagenet.py:371-429).
+"""End-to-end training runs of the CLI on the HIP path (imagenet.py:113-131 hot loop, :371-429 driver).
 
-A learnable synthetic task (``--synthetic-task colour``: 10 classes, each a
-mean colour + stripe orientation + noise, 64x64) replaces ImageNet, which is
-not available here, so convergence parity with the reference's published
-100-epoch curve stays unpinned; what is checked is that the bf16 HIP path
-LEARNS like the fp32 PyTorch path does on the same task:
+A learnable synthetic task (``--synthetic-task colour``: 10 classes, each a mean colour + stripe orientation +
+noise, 64x64) replaces ImageNet, which is not available here, so parity with the reference's published 100-epoch
+curve stays unpinned. ResNet-18, batch 32, lr 0.05 (half an epoch of warmup) is a CHAOTIC regime for every
+numerics path: profiles/trajectory_r18_b32.md shows the fp32 PyTorch oracle itself passing through loss spikes
+(a 10-step mean of 13.1 in one lockstep run), and a HIP run, a PyTorch fp32 run and a PyTorch bf16-autocast run
+started from one state drifting apart at the same rate. Two runs of different paths are therefore NOT compared
+curve against curve; the tests check instead:
 
-* default CLI path: iteration-1 bucket rebuild + ``native.rebind()``, RCCL
-  self-collectives, wgrad side stream, folded-BN validation, ``--save-model``
-  (122-key reference-layout checkpoint), ``--checkpoint-dir`` then
-  ``--resume`` for a third epoch;
-* ``--accum-steps 2`` and ``--dtype fp8`` variants;
-* the fp32 ``--kernels torch`` oracle on the same data and seed.
+* along the HIP trajectory, every step against PyTorch recomputing the same step on the HIP weights
+  (``scripts/trajectory_diff.py``): gradients, loss, SGD update, bf16 shadows, BN running statistics, the
+  folded-BN eval forward, and the parameter drift from the fp32 trajectory, each against what bf16 autocast
+  gives (the yardstick: the reference trains fp32, a bf16 path is expected to match autocast, not fp32);
+* that the CLI learns, checkpoints (122-key reference layout) and resumes, with the reference's step LR
+  decay (x0.1, imagenet.py:154-162) brought forward to epoch 3 so the last epoch is out of the chaotic
+  regime; the same for ``--accum-steps 2``, ``--dtype fp8`` and the ``IMAGENT_BN_SHIFT=0`` switch.
 """
 
+import json
 import math
 import os
 import re
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 import torch
 
@@ -28,94 +33,117 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 BASE = ["--arch", "resnet18", "--image-size", "64", "--data", "synthetic", "--synthetic-task", "colour",
         "--num-classes", "10", "--batch-size", "32", "--synthetic-train-size", str(32 * 150),
-        "--synthetic-val-size", "1024", "--lr", "0.05", "--log-interval", "10", "--quiet-banner",
-        "--tb-dir", ""]
+        "--synthetic-val-size", "1024", "--lr", "0.05", "--warmup-epochs", "0.5", "--log-interval", "10",
+        "--quiet-banner", "--tb-dir", ""]
+# the reference's step decay, brought forward: epochs 1-2 at lr 0.05, epoch 3 at 0.005
+DECAY = ["--lr-step", "2"]
+CHANCE = math.log(10)
+
+
+def _env(**extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, **extra)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    return env
 
 
 def _run(args, cwd, timeout=400, **extra_env):
-    env = dict(os.environ, PYTHONPATH=ROOT, **extra_env)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
-        env.pop(k, None)
-    r = subprocess.run([sys.executable, "-u", "-m", "imagent_amd.cli"] + args, cwd=cwd, env=env,
+    r = subprocess.run([sys.executable, "-u", "-m", "imagent_amd.cli"] + args, cwd=cwd, env=_env(**extra_env),
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-4000:]
     return r.stdout
 
 
 def _curve(out):
-    first = [float(m) for m in re.findall(r"iter \d+/\d+ loss ([0-9.naninf]+)", out)]
-    summ = [(float(a), float(b)) for a, b in re.findall(r"Train loss: ([0-9.e+-]+) ; Test loss: ([0-9.e+-]+)", out)]
+    summ = [(float(a), float(b)) for a, b in re.findall(r"Train loss: ([0-9.e+-]+|nan|inf) ; Test loss: ([0-9.e+-]+|nan|inf)", out)]
     top1 = [float(v) for v in re.findall(r"; Test top1 accuracy: ([0-9.e+-]+)", out)]
-    return first, summ, top1
+    return summ, top1
 
 
-# half an epoch of LR warmup for the HIP-vs-oracle comparison: without it both paths pass through an
-# early loss spike whose size and timing are chaotic (profiles/convergence_r50.md), e.g. an oracle run
-# measured at 2.00 / 0.46 epoch means against the HIP run's 0.49 / 0.002
-WARM = ["--warmup-epochs", "0.5"]
-# the variant / A-B-switch tests only ask "does it learn": at lr 0.05 a run can still leave the basin after
-# it has learned the task (measured: accum2 epoch means 0.65 -> 1.59; IMAGENT_BN_SHIFT=0 1.47 -> 3.79 over
-# 40 iterations, both passing on other runs of the same build), so they train at a calmer lr. The fp32
-# PyTorch oracle does the same at lr 0.05 with --accum-steps 2 (last-epoch train loss 1.06 / 0.29 / 1.21 over
-# three seeds, 71.1 % validation top-1 on one; profiles/convergence_r50.md, round-4 table)
-CALM = ["--lr", "0.02"]
+def _learned(summ, top1, out):
+    """The last epoch (lr 0.005) has learned the task: validation top-1 above 90 % and a mean train loss under a
+    third of chance level; every epoch finite."""
+    assert summ and all(math.isfinite(a) and math.isfinite(b) for a, b in summ), out[-3000:]
+    assert top1[-1] > 90.0 and summ[-1][0] < CHANCE / 3, (summ, top1)
 
 
-def test_hip_training_converges_saves_and_resumes(tmp_path):
-    # at the calmer lr of the variant tests, for the HIP run and the oracle alike: at lr 0.05 a HIP run of the round-5
-    # final build passed through the chaotic early spike (epoch means 2.78 / 1.51, validation loss 6.81 / 0.017:
-    # the task learned, the epoch-2 train mean still carrying the spike) where the run before on the same kernels
-    # had not; judged against the chance-level loss ln 10, not the first logged interval (runs differ in how much
-    # of the task they have learned by iteration 10: 1.88 in that run)
-    out = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "2", "--save-model", "--checkpoint-dir",
-                                     str(tmp_path)], tmp_path)
-    first, summ, top1 = _curve(out)
+def test_hip_steps_track_pytorch_along_the_hip_trajectory(tmp_path):
+    out = tmp_path / "traj.jsonl"
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "scripts", "trajectory_diff.py"), "--lockstep",
+                        "--out", str(out), "--"] + BASE + ["--epochs", "2"], cwd=tmp_path, env=_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:]
+    recs = [json.loads(line) for line in open(out)][1:]
+    steps = [x for x in recs if "step" in x]
+    vals = [x for x in recs if x.get("validate")]
+    assert len(steps) == 300 and len(vals) == 2, r.stdout[-3000:]
+    assert all(math.isfinite(x["loss_hip"]) and math.isfinite(x["gerr_hip"]) for x in steps)
+
+    # gradients: relative error against fp32 PyTorch on the same weights, HIP vs bf16 autocast, over the steps that
+    # move the weights (fp32 gradient norm >= 1 % of the run's RMS: at a loss ~1e-5 the gradient is ~1e-4 and its
+    # relative error is rounding of a vanishing quantity)
+    n = np.array([x["gnorm_fp32"] for x in steps])
+    keep = n >= 1e-2 * np.sqrt((n ** 2).mean())
+    h = np.array([x["gerr_hip"] for x in steps])[keep]
+    b = np.array([x["gerr_bf16"] for x in steps])[keep]
+    assert keep.sum() >= 100
+    win = [np.sqrt((h[i:i + 10] ** 2).sum() / (b[i:i + 10] ** 2).sum()) for i in range(0, len(h), 10)]
+    assert max(win) <= 2.0, win                                  # every 10-step window: <= 2x autocast's error
+    assert np.sqrt((h ** 2).sum() / (b ** 2).sum()) <= 1.25      # the whole run: autocast's level
+    assert (h / b).max() <= 5.0, (h / b).max()                   # no single gross step
+    # the loss on the same weights
+    for x in steps:
+        d = abs(x["loss_hip"] - x["loss_fp32"])
+        assert d <= max(3 * abs(x["loss_bf16"] - x["loss_fp32"]), 0.01 + 0.01 * x["loss_fp32"]), x
+    # the SGD step is torch.optim.SGD's (imagenet.py:325) from the same (P, G, momentum); shadows = bf16(P) exactly
+    assert max(x["sgd_step_err"] for x in steps) <= 1e-4
+    assert max(x["shadow_err"] for x in steps) <= 1e-6
+    # BN running statistics after each step (shifted-sum batch statistics, unbiased running variance)
+    for x in steps:
+        assert x["bn_rvar_err_hip"] <= 2 * x["bn_rvar_err_bf16"] + 1e-6, x
+        assert x["bn_rmean_err_hip"] <= 2 * x["bn_rmean_err_bf16"] + 1e-6, x
+    # the folded-BN eval forward gives what PyTorch's eval forward gives on the same weights / running statistics
+    for v in vals:
+        assert abs(v["hip_val_loss"] - v["torch_eval_val_loss"]) <= 0.02 * max(abs(v["torch_eval_val_loss"]), 0.5), v
+        assert abs(v["hip_val_top1"] - v["torch_eval_val_top1"]) <= 1.0, v
+    # drift: the HIP trajectory leaves the fp32 one no faster than the bf16-autocast trajectory does
+    for x in steps:
+        assert x["dist_hip_fp32"] <= 2 * x["dist_bf16_fp32"] + 1e-4, x
+
+
+def test_hip_training_learns_saves_and_resumes(tmp_path):
+    out = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "2", "--save-model", "--checkpoint-dir",
+                               str(tmp_path)], tmp_path)
+    summ, top1 = _curve(out)
     assert len(summ) == 2 and len(top1) == 2, out[-3000:]
-    assert first[0] > 0.5 and all(math.isfinite(v[0]) for v in summ), (first, summ)
-    assert summ[-1][0] < 2.303 / 3, (first[0], summ)  # last-epoch train loss under a third of chance level
-    assert top1[-1] > 90.0, top1
+    assert all(math.isfinite(a) and math.isfinite(b) for a, b in summ), summ
+    # above chance at some point of the chaotic lr-0.05 phase (the saved best model); the learning check is epoch 3
+    assert max(top1) > 50.0, top1
     # reference-layout best checkpoint: 122 keys with the DDP 'module.' prefix
     sd = torch.load(tmp_path / "imagenet_FR_resnet18.pt", map_location="cpu", weights_only=True)
     assert len(sd) == 122 and all(k.startswith("module.") for k in sd)
-    # resume for epoch 3
-    out2 = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "3", "--resume",
-                                      str(tmp_path / "state_resnet18.pt")], tmp_path)
+    # resume for epoch 3 (lr 0.005)
+    out2 = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "3", "--resume", str(tmp_path / "state_resnet18.pt")],
+                tmp_path)
     assert "Resumed from" in out2 and "Epoch 3 Summary: " in out2 and "Epoch 1 Summary" not in out2
-    _, summ2, top1_2 = _curve(out2)
-    assert top1_2[-1] > 90.0 and summ2[-1][0] < 2.303 / 3, (summ2, top1_2)
-
-    # the fp32 PyTorch oracle on the same task / seed learns the same way
-    ref = _run(BASE + WARM + CALM + ["--kernels", "torch", "--dtype", "fp32", "--epochs", "2"], tmp_path)
-    rfirst, rsumm, rtop1 = _curve(ref)
-    assert rtop1[-1] > 90.0
-    # stated band: the last epoch's mean train loss of the HIP run is at most the oracle's + 0.15
-    # (absolute) + 50 % (one-sided: the HIP run ending lower is not a failure; epoch 1 is not compared)
-    assert summ[-1][0] - rsumm[-1][0] < 0.15 + 0.5 * rsumm[-1][0], (summ, rsumm)
+    assert "Learning rate: 0.005" in out2
+    summ2, top1_2 = _curve(out2)
+    _learned(summ2, top1_2, out2)
 
 
 @pytest.mark.parametrize("extra", [["--accum-steps", "2"], ["--dtype", "fp8"]], ids=["accum2", "fp8"])
-def test_hip_training_variants_converge(tmp_path, extra):
-    out = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "2"] + extra, tmp_path)
-    first, summ, top1 = _curve(out)
-    assert len(top1) == 2, out[-3000:]
-    # an epoch mean under a third of the chance-level loss ln 10 (the first logged interval is no
-    # reference: some runs have learned most of the task by iteration 10). The BEST epoch: on this toy task an
-    # fp8 run has also learned it (epoch-1 mean 0.45) and then left the basin in epoch 2 (mean 1.19) with the
-    # same build that passed the run before -- the chaotic tail the comment above describes, not a numerics
-    # regression; the last epoch must still be finite
-    k = min(range(len(summ)), key=lambda i: summ[i][0])
-    assert summ[k][0] < 2.303 / 3, (first, summ)
-    assert top1[k] > 90.0, top1
-    assert all(math.isfinite(v[0]) for v in summ), summ
+def test_hip_training_variants_learn(tmp_path, extra):
+    out = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "3"] + extra, tmp_path)
+    summ, top1 = _curve(out)
+    assert len(top1) == 3, out[-3000:]
+    _learned(summ, top1, out)
 
 
 def test_bn_shift_off_switch_trains(tmp_path):
     """IMAGENT_BN_SHIFT=0 (forward BN statistics as raw sums, an A/B switch): the finalize must not
     add the previous batch mean back (it did: NaN losses from the second step on)."""
-    # (with half an epoch of LR warmup, as the other trainer tests: without it an early run can pass through
-    # a chaotic phase -- one measured 1.12 -> 1.71 -> 1.45 -> 2.41 over the epoch's logged intervals)
-    out = _run(BASE + WARM + CALM + ["--kernels", "hip", "--epochs", "1", "--synthetic-train-size", str(32 * 40)],
+    out = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "3", "--synthetic-train-size", str(32 * 40)],
                tmp_path, IMAGENT_BN_SHIFT="0")
-    first, summ, top1 = _curve(out)
-    assert len(summ) == 1 and all(v == v for v in first) and summ[0][0] == summ[0][0], out[-2000:]
-    assert summ[0][0] < 2.0, (first, summ)  # learning: the epoch mean is below chance level (ln 10 = 2.30)
+    summ, top1 = _curve(out)
+    assert len(summ) == 3, out[-2000:]
+    _learned(summ, top1, out)
