@@ -24,6 +24,7 @@
 // registers, loads/stores are 16 B per lane (cdna_hip_programming.md G13).
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -89,6 +90,12 @@ __device__ __forceinline__ void st8(bf16_t* p, const Vec8& x) {
 // packed 16-B row chunk: load, element i as f32, store (NT: non-temporal -- the streamed output
 // is read back by the next kernel only after far more than the L2 / MALL has passed through)
 __device__ __forceinline__ u32x4 ldw(const bf16_t* p) { return *reinterpret_cast<const u32x4*>(p); }
+// non-temporal load of a streamed operand (read once; scripts/hbm_roof.hip: r2w1 6.32 vs 5.92 TB/s plain)
+template <bool NTL>
+__device__ __forceinline__ u32x4 ldwn(const bf16_t* p) {
+    if (NTL) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return *reinterpret_cast<const u32x4*>(p);
+}
 __device__ __forceinline__ float bfw(const u32x4& w, int i) { return (i & 1) ? hi_bf(w[i >> 1]) : lo_bf(w[i >> 1]); }
 template <bool NT>
 __device__ __forceinline__ void stw(bf16_t* p, const u32x4& w) {
@@ -624,7 +631,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // residual gradient g, MODE 2 the downsample-branch input gradient. Block 0 also adds the sums into
 // the arena slots of dgamma/dbeta (+= : gradient accumulation). Rows stay packed bf16 words until
 // their math and the per-channel constants are three FMAs' worth (108 -> fewer VGPRs, more waves).
-template <int MASK, int MODE, bool NT, bool Q8>
+template <int MASK, int MODE, bool NT, bool Q8, bool NTL = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -684,10 +691,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         for (int u = 0; u < UB; ++u) {
             // clamped row, unconditional loads (see bn_fwd_kernel); rows past R are not stored
             const size_t off = (size_t)min(r0 + u * step, R - 1) * C + c0;
-            g[u] = ldw(dy + off);
-            xv[u] = ldw(x + off);
-            if (MODE == 2) x2v[u] = ldw(x2 + off);
-            if (MASK == 1) yv[u] = ldw(y + off);
+            g[u] = ldwn<NTL>(dy + off);
+            xv[u] = ldwn<NTL>(x + off);
+            if (MODE == 2) x2v[u] = ldwn<NTL>(x2 + off);
+            if (MASK == 1) yv[u] = ldwn<NTL>(y + off);
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
@@ -759,6 +766,34 @@ int resident_grid(const void* kernel, int grid) {
         it = cap.emplace(kernel, per_cu * ncu).first;
     }
     return grid < it->second ? grid : it->second;
+}
+
+// backward apply pass: blocks per CU of its grid and non-temporal operand loads. The streaming roof of the r2w1
+// pattern (g, x in; dx out) is highest at LOW occupancy with NT accesses (scripts/hbm_roof.hip, profiles/
+// hbm_roof.md: 6.32 TB/s at 2 blocks / CU vs 5.7-5.8 at 8). Round 6, same box, bench.py at 2048 img: 8 blocks / CU
+// plain loads 17,351 / 17,363 img/s, 2 + NT 17,458 / 17,478, 4 + NT 17,541 (scripts/bn_bench.py: bwd apply per
+// step 25.15 -> 23.75 ms). IMAGENT_BN_APPLY_BPC / IMAGENT_BN_NTLOAD override.
+static int env_int(const char* k, int d) {
+    const char* v = getenv(k);
+    return v && *v ? atoi(v) : d;
+}
+static int apply_bpc() {
+    static const int v = env_int("IMAGENT_BN_APPLY_BPC", 4);
+    return v;
+}
+static bool apply_ntload() {
+    static const bool v = env_int("IMAGENT_BN_NTLOAD", 1) != 0;
+    return v;
+}
+static int n_cus() {
+    static const int n = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        return cus;
+    }();
+    return n;
 }
 
 int grid_for(long R, int C) {
@@ -864,19 +899,20 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
                            BWD_SLOTS, 3 * C);
         IMK_CHECK_LAUNCH();
     }
-    const int grid = std::max(grid_for(R, C), fold_in ? (3 * C + 255) / 256 : 1);
+    const int grid = std::max(std::min(grid_for(R, C), apply_bpc() * n_cus()), fold_in ? (3 * C + 255) / 256 : 1);
     const float inv_cnt = 1.f / (float)R;
-    const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1];
-#define LK(M, NT, Q8)                                                                                \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8>),                                               \
-                       dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
+    const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1], ntl = apply_ntload();
+#define LK(M, NT, Q8, NTL)                                                                           \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8, NTL>),                                          \
+                       dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8, NTL>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
                        nullptr, (const bf16_t*)x, save, gamma, nullptr, folded, (bf16_t*)dx, nullptr,       \
                        (const bf16_t*)x2, save2, gamma2, (bf16_t*)dx2, dgamma_acc, dbeta_acc,               \
                        dgamma2_acc, dbeta2_acc, R, C, inv_cnt, g8, sgx_row * C, fold)
 #define LA(M)                                                                  \
     do {                                                                       \
-        if (q8) { if (nt) LK(M, true, true); else LK(M, false, true); }        \
-        else { if (nt) LK(M, true, false); else LK(M, false, false); }         \
+        if (q8) { if (nt) LK(M, true, true, false); else LK(M, false, true, false); }        \
+        else if (ntl) LK(M, true, false, true);                                \
+        else { if (nt) LK(M, true, false, false); else LK(M, false, false, false); }         \
     } while (0)
     if (mode == 2) LA(2); else LA(0);
 #undef LK

@@ -132,6 +132,19 @@ int main(int argc, char** argv) {
     CK(hipMemset(a, 0x3c, n * 16));
     CK(hipMemset(b, 0x3c, n * 16));
     CK(hipMemset(o, 0, n * 16));
+    if (argc > 2 && argv[2][0] == 'c') {  // counter calibration: one launch per pattern, known bytes
+        double m;
+        printf("calibration launches (GiB per stream %.2f): read, write, copy, r2w1 (plain), then NT\n", gib);
+        run<0, 8, false>(a, b, o, n, sink, 4 * cus, &m);
+        run<1, 8, false>(a, b, o, n, sink, 4 * cus, &m);
+        run<2, 8, false>(a, b, o, n, sink, 4 * cus, &m);
+        run<3, 8, false>(a, b, o, n, sink, 4 * cus, &m);
+        run<0, 8, true>(a, b, o, n, sink, 4 * cus, &m);
+        run<1, 8, true>(a, b, o, n, sink, 4 * cus, &m);
+        run<2, 8, true>(a, b, o, n, sink, 4 * cus, &m);
+        run<3, 8, true>(a, b, o, n, sink, 4 * cus, &m);
+        return 0;
+    }
     printf("%d CUs, %.1f GiB per stream; TB/s best / median of 10 reps (reads + writes)\n\n", cus, gib);
     printf("| pattern | blocks/CU | U4 | U8 | U16 | U4 NT | U8 NT | U16 NT |\n|---|---:|---:|---:|---:|---:|---:|---:|\n");
     sweep<0>("read", a, b, o, n, sink, cus);

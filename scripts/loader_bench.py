@@ -113,6 +113,7 @@ def main():
     a = ap.parse_args()
     rows = []
     d = a.dir or tempfile.mkdtemp(prefix="imrec_")
+    os.makedirs(d, exist_ok=True)
     # "448@320": 448^2 model input from records stored at 320^2 (GPU resample, --record-resize)
     for spec in a.sizes.split(","):
         size, stored = (int(v) for v in spec.split("@")) if "@" in spec else (int(spec), int(spec))
