@@ -26,6 +26,11 @@ def short(name):
     return n.split("(")[0]
 
 
+# FETCH_SIZE counts half of the bytes read on MI355X / ROCm 7 (profiles/hbm_roof.md: calibrated on kernels that move a
+# known 1 GiB: FETCH_SIZE 524,305 for 1,048,576 KiB read; WRITE_SIZE exact in KiB)
+FETCH_UNIT = 2048
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
@@ -38,7 +43,7 @@ def main():
     for n, v, t in fr:
         g = agg[short(n)]
         g[0] += 1
-        g[1] += v * 1024
+        g[1] += v * FETCH_UNIT
         g[3] += t
     for n, v, _ in wr:
         agg[short(n)][2] += v * 1024
