@@ -75,13 +75,15 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--arch", default="resnet50")
-    # 2048/GPU: the per-GPU batch sized for 288 GB of HBM (~0.06 GiB reserved per image: ~110 GiB). It fills
-    # the chip on the 7x7/14x14 stages and halves the all-reduce's share of each step against 1024 (same box,
-    # round 5: 2048 16,498 / 16,522 img/s vs 1024 16,087 / 16,094; 1536 in between; 256: -15 %, 512: -4 %
-    # vs 1024). Layer-1 activations pass 2^31 bytes at this batch: every kernel's buffer descriptors are
-    # tile / split / band based (tests/test_large_tensors_gpu.py)
+    # 4096/GPU: the per-GPU batch sized for 288 GB of HBM (142.5 GiB peak, 186 GiB reserved: ~0.0455 GiB per image).
+    # It fills the chip on the 7x7/14x14 stages and shrinks the all-reduce's and the per-step fixed costs' share
+    # (round 5: 2048 16,498 / 16,522 img/s vs 1024 16,087 / 16,094; round 6, two boxes, alternating: 4096 17,610 /
+    # 17,558 vs 2048 17,424 / 17,469, and 17,511 / 17,487 vs 17,354 / 17,390). The stem output and the layer-1
+    # tensors hold 3.3 G elements (6.6 GB) at this batch: every kernel's buffer descriptors are tile / split / band
+    # based and a duplicated-batch training step matches bit for bit per half
+    # (tests/test_large_tensors_gpu.py::test_train_step_4096_duplicated_halves)
     ap.add_argument("--batch-size", type=int, default=None,
-                    help="per GPU (default 2048; halved down to 256 when the device has too little free HBM)")
+                    help="per GPU (default 4096; halved down to 256 when the device has too little free HBM)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--kernels", default="hip", choices=["hip", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=16.0)
@@ -142,20 +144,19 @@ def main(argv=None):
         torch.cuda.set_per_process_memory_fraction(float(os.environ["IMAGENT_MEM_FRACTION"]), ctx.device)
     auto_reduced = False
     if a.batch_size is None:
-        a.batch_size = 2048
+        a.batch_size = 4096
         if ctx.device.type == "cuda" and ctx.world_size == 1:
             # a GPU shared with another job (seen on the dev pool: a neighbour holding up
-            # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.052 GiB
-            # per image (52.7 GiB at 1024, profiles/r50_b1024_allocator.md) + 15 % headroom, and
-            # below that it thrashes (hipMalloc retries every step). Multi-rank runs keep
-            # the default on every rank.
+            # to 283 of the 288 GB) cannot fit the default: the allocator reserves ~0.0455 GiB
+            # per image (186 GiB at 4096, 93.4 at 2048) + 15 % headroom, and below that it
+            # thrashes (hipMalloc retries every step). Multi-rank runs keep the default on every rank.
             free = torch.cuda.mem_get_info(ctx.device)[0] / 2**30
             frac = os.environ.get("IMAGENT_MEM_FRACTION")
             if frac:
                 free = min(free, float(frac) * torch.cuda.get_device_properties(ctx.device).total_memory / 2**30)
-            while a.batch_size > 256 and 0.06 * a.batch_size > free:
+            while a.batch_size > 256 and 0.0525 * a.batch_size > free:
                 a.batch_size //= 2
-            if a.batch_size != 2048:
+            if a.batch_size != 4096:
                 auto_reduced = True
                 print(f"bench: {free:.1f} GiB of HBM free, running {a.batch_size} img/GPU", file=sys.stderr,
                       flush=True)
