@@ -161,13 +161,21 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     // 1x1 convs keep the persistent grid and its epilogue/prefetch overlap
     const bool use_lds = lds_ok && !(a.flags & IG_EPI_DIRECT) &&
                          (bnb || (a.flags & IG_EPI_LDS) || (K + BK - 1) / BK > 4);
-    if (tile == 17 || tile == 18 || tile == 19 || tile == 27 || tile == 28) {  // v3 main loop (conv_igemm_v3.h); 19: 256x128; 27 / 28: tap-inner
+    if (tile == 17 || tile == 18 || tile == 19 || tile == 27 || tile == 28 || (tile >= 29 && tile <= 32)) {
+        // v3 main loop (conv_igemm_v3.h); 19: 256x128; 27 / 28: tap-inner; 29-32: deeper rings (round 6 A/B: the
+        // 2-deep ring waits vmcnt(0) at every stage, so one stage of MFMA time must cover the fill latency):
+        // 29 256x256 BK 32 x 4 (3 fills in flight, 128 KB), 30 256x256 BK 32 x 3, 31 128x128 BK 32 x 4 (64 KB,
+        // two blocks / CU), 32 128x128 BK 64 x 3 (96 KB, one block / CU)
         if (!use_lds || !v3_ok(a)) return -105;
         switch (tile) {
             case 17: return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
             case 19: return launch_v3<256, 128, 2, 2, 8, 128>(a, st);
             case 18: return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
             case 27: return launch_v3<256, 256, 2, 2, 8, 128, 2, 0, true>(a, st);
+            case 29: return launch_v3<256, 256, 2, 4, 8, 64>(a, st);
+            case 30: return launch_v3<256, 256, 2, 3, 8, 64>(a, st);
+            case 31: return launch_v3<128, 128, 2, 4, 4, 64>(a, st);
+            case 32: return launch_v3<128, 128, 2, 3, 4, 128>(a, st);
             default: return launch_v3<128, 128, 2, 2, 4, 128, 2, 0, true>(a, st);
         }
         // (a 16-wave 256x256 tile of 64 x 64 waves, round 5: no faster than these on any R50 shape, its staged BN-backward
