@@ -183,6 +183,19 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
     }
     if (autotile && use_lds && md == 0 && a.Nout >= 128 && v3_ok(a)) {
         const long t8 = (long)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+        // forward-type convs (BN statistics or the eval BN affine in the epilogue, no fused BN backward): 32-deep
+        // stages with 2-3 fills in flight instead of 64-deep x 2 (whose vmcnt(0) at every stage leaves one stage of
+        // MFMA time to cover the fill latency). Round 6, isolated at 2048 img (scripts/runs/ring_ab.sh, tiles 30 / 31
+        // vs 17 / 18): forwards 256@14 3x3 554 -> 502 us, 1024 -> 256 @14 346 -> 325, 512@7 3x3 521 -> 491, 256@28
+        // 3x3 s2 642 -> 567, 128@28 3x3 721 -> 665, 512 -> 128 @28 570 -> 498; the dgrads (plain or with the fused
+        // BN backward) gain nothing (-3 .. +2 %). In-step at 4096 img the isolated gain does NOT carry over:
+        // 17,317 / 17,289 img/s with it vs 17,358 / 17,395 without, alternating on one box -- so it stays OFF by
+        // default; IMAGENT_V3_DEEP=1 turns it on (A/B), tiles 29-32 remain as tested explicit variants
+        static const bool deep = [] {
+            const char* e = getenv("IMAGENT_V3_DEEP");
+            return e && atoi(e) != 0;
+        }();
+        const bool fwd_ring = deep && !bnb && (a.stats || (a.flags & IG_AFFINE));
         // (the fused BN-backward dgrads on 128x128 tiles with their epilogue operands prefetched instead: within
         // +-5 % per shape, profiles/r50_b1024_round4_kernel_ab.md -- not taken; again at 2048 img in round 5, isolated
         // 2-7 % faster, in-step 16,584 / 16,576 vs 16,612 / 16,621 img/s)
@@ -193,15 +206,16 @@ IMK_EXPORT int imk_conv_igemm(const IGemmArgs* args, int tile, void* stream) {
                 m.N = i1;
                 m.M = i1 * a.OH * a.OW;
                 advance_images(t, a, i1);
-                const int r = launch_v3<256, 256, 2, 2, 8, 128>(m, st);
-                return r != 0 ? r : launch_v3<128, 128, 2, 2, 4, 128>(t, st);
+                const int r = fwd_ring ? launch_v3<256, 256, 2, 3, 8, 64>(m, st) : launch_v3<256, 256, 2, 2, 8, 128>(m, st);
+                if (r != 0) return r;
+                return fwd_ring ? launch_v3<128, 128, 2, 4, 4, 64>(t, st) : launch_v3<128, 128, 2, 2, 4, 128>(t, st);
             }
-            return launch_v3<256, 256, 2, 2, 8, 128>(a, st);
+            return fwd_ring ? launch_v3<256, 256, 2, 3, 8, 64>(a, st) : launch_v3<256, 256, 2, 2, 8, 128>(a, st);
         }
         // (256x128 tiles on 8 waves for the 128-channel outputs, tile 19, round 5: forward 3-6 % faster stand-alone,
         // dgrad 6 % and the fused BN-backward dgrads 7-21 % slower, in-step 16,822 / 16,842 vs 17,003 / 16,991 img/s
         // -- not taken, profiles/r50_b2048_r5_v3_256x128.md)
-        return launch_v3<128, 128, 2, 2, 4, 128>(a, st);
+        return fwd_ring ? launch_v3<128, 128, 2, 4, 4, 64>(a, st) : launch_v3<128, 128, 2, 2, 4, 128>(a, st);
     }
     if (bnb || use_lds) {  // the tiles the auto choice makes, with a fused / staged epilogue
         if (regstage || (tile != 2 && tile != 8)) {
