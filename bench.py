@@ -98,7 +98,8 @@ def main(argv=None):
     ap.add_argument("--bn-fusion", type=int, default=1, help="0: separate BN-backward reduce pass")
     ap.add_argument("--wgrad-overlap", type=int, default=1, help="0: weight gradients on the main stream")
     ap.add_argument("--graph", type=int, default=0,
-                    help="1: capture the whole step in a HIP graph and replay it (1 GPU; launch-bound small batches)")
+                    help="1: capture the whole step in a HIP graph and replay it (1 GPU; launch-bound small batches); "
+                         "2: also capture the weight-gradient side stream")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars"],
                     help="lars: layer-wise adaptive rates for the large-batch (8192) configuration")
     ap.add_argument("--eval", type=int, default=0,
@@ -229,7 +230,7 @@ def main(argv=None):
             if ctx.world_size > 1:
                 raise SystemExit("--graph is validated for one GPU only")
             from imagent_amd.train.engine import GraphedStep
-            one = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr)
+            one = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr, two_stream=a.graph == 2)
 
         def steps(n):
             for u8, y in src.batches(n):

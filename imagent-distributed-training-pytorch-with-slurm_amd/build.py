@@ -108,6 +108,27 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     return out
 
 
+def build_kernels_variant(tag: str, defines: List[str], jobs: int = 8) -> str:
+    """An A/B build of the kernels library with extra compile flags (e.g. ``-DEPI_QB=4``) into
+    ``_native/ab/<tag>/``; a process loads it instead of the default with ``IMAGENT_KERNELS_LIB=<path>``."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    d = os.path.join(OUT, "ab", tag)
+    out = os.path.join(d, "libimagent_kernels.so")
+    key = ["kernels", ARCH] + HIP_FLAGS + list(defines)
+    if not _stale(srcs + hdrs, out, key):
+        return out
+    os.makedirs(os.path.join(d, "obj"), exist_ok=True)
+    objs = [os.path.join(d, "obj", os.path.basename(x) + ".o") for x in srcs]
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(lambda so: _compile_hip_object(so[0], so[1], list(defines)), zip(srcs, objs)))
+    tl = _torch_lib_dir()
+    _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs +
+         [f"-L{tl}", f"-Wl,-rpath,{tl}"])
+    _stamp(srcs + hdrs, out, key)
+    return out
+
+
 def build_comm(force: bool = False) -> str:
     src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
     out = os.path.join(OUT, "libimagent_comm.so")

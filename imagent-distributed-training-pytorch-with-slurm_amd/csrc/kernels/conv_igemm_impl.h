@@ -449,6 +449,13 @@ __host__ __device__ constexpr int epi_red_stride(int BN, int NT) {
     return (NT / (BN / 8)) * (BN / 8) + ((BN / 8) < 32 ? (BN / 8) : 0);
 }
 
+// staged-epilogue chunks per thread whose global reads (x, mask bits, accumulate operand) are issued together: 4.
+// (Round 6 A/B with 8 for the 256-row tiles -- 2 round trips instead of 4, 241 VGPRs, no spills: dgrad + BN backward
+// within +-2 % isolated, in-step 17,497 / 17,515 vs 17,511 / 17,484 img/s: not kept.) -DEPI_QB=n overrides (A/B builds)
+#ifndef EPI_QB
+#define EPI_QB 0
+#endif
+
 template <int BM, int BN, int NT>
 struct EpiPF {
     static constexpr int CPR = BN / 8, RG = NT / CPR, NQ = BM / RG;
@@ -579,7 +586,7 @@ __device__ __forceinline__ void epilogue_lds_put(const IGemmArgs& a, Put put, ch
     // without the two runtime divisions per row chunk of the general (strided-dgrad phase / padded) map
     const bool dense = epi_dense(a);
     const bool pfon = pf && pf->on;  // x / mask bits already in registers (epi_prefetch)
-    constexpr int QB = 4;  // chunks whose global reads are issued together
+    constexpr int QB = EPI_QB > 0 ? EPI_QB : 4;  // chunks whose global reads are issued together
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += QB) {
         long e[QB];

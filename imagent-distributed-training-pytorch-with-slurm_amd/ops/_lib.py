@@ -25,6 +25,8 @@ class NativeLibraryMissing(RuntimeError):
 
 
 def _path(name: str) -> str:
+    if name == "kernels" and os.environ.get("IMAGENT_KERNELS_LIB"):  # A/B builds (build.build_kernels_variant)
+        return os.environ["IMAGENT_KERNELS_LIB"]
     return os.path.join(_NATIVE, f"libimagent_{name}.so")
 
 

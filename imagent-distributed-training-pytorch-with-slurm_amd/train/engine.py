@@ -142,8 +142,13 @@ class GraphedStep:
     re-captures. Host-side counters are not advanced by replays.
     """
 
-    def __init__(self, fn, warmup: int = 3, key_fn=None):
+    def __init__(self, fn, warmup: int = 3, key_fn=None, two_stream: bool = False):
         self.fn, self.warmup, self.key_fn = fn, warmup, key_fn
+        # two_stream: capture the weight-gradient side stream too (its fork / join become event edges of the
+        # graph); default off: on ROCm 7 / torch 2.10 a replayed two-branch graph measured slower than eager
+        # (profiles/r50_small_batch_graph_r5.md) and the round-1 / round-5 captures segfaulted in EndCapture on
+        # ResNet-18's deterministic mode (scripts/graph_capture_repro.py)
+        self.two_stream = two_stream
         self.graph = None
         self.static = None
         self.key = None
@@ -175,7 +180,7 @@ class GraphedStep:
         # hipStreamEndCapture on this ROCm 7 / torch 2.10 stack, even with the
         # join made explicit -- measured in round 1 (capture experiment)
         overlap = streams.overlap_enabled()
-        streams.set_wgrad_overlap(False)
+        streams.set_wgrad_overlap(overlap and self.two_stream)
         try:
             with torch.cuda.graph(g):
                 self.fn(*self.static)

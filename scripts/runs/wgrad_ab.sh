@@ -8,3 +8,6 @@ for v in 1 2 3 1 2 3; do
   echo "wgrad_v3=$v $(grep '"metric"' $O/bench_$v.log | cut -c60-130)" >> $O/bench_summary.log
 done
 timeout -k 10 300 python -u scripts/bn_bench.py --batch 256 > $O/bn_bench_256.log 2>&1 || exit 1
+# two-stream graph capture repro (R18 deterministic, the round-1 / round-5 crash config; then R50 non-deterministic)
+timeout -k 10 240 python -u -X faulthandler scripts/graph_capture_repro.py --arch resnet18 --deterministic 1 --batch 64 > $O/graph_r18_det.log 2>&1; rc=$?; echo "rc=$rc" >> $O/graph_r18_det.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 240 python -u -X faulthandler scripts/graph_capture_repro.py --arch resnet50 --deterministic 0 --batch 128 > $O/graph_r50.log 2>&1; rc=$?; echo "rc=$rc" >> $O/graph_r50.log; [ $rc -eq 0 ] || exit 1

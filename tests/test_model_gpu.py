@@ -277,6 +277,27 @@ def test_graphed_step_matches_eager_deterministic():
     assert e < 1e-3, e
 
 
+def test_graphed_two_stream_step_matches_eager():
+    """GraphedStep(two_stream=True): the weight-gradient side stream captured too (fork / join as event edges of
+    the graph) -- the round-1 / round-5 configuration that segfaulted in hipStreamEndCapture; at HEAD it captures
+    and replays (scripts/graph_capture_repro.py, profiles/r50_small_batch_graph_r6.md) and must update like eager."""
+    worst, e = _graphed_vs_eager(two_stream=True)
+    assert worst < 0.1, worst
+    assert e < 0.5, e
+
+
+def test_graphed_two_stream_step_matches_eager_deterministic():
+    from imagent_amd.ops import conv as cv
+    prev = cv.deterministic()
+    cv.set_deterministic(True)
+    try:
+        worst, e = _graphed_vs_eager(two_stream=True)
+    finally:
+        cv.set_deterministic(prev)
+    assert worst < 1e-3, worst
+    assert e < 1e-3, e
+
+
 def test_deterministic_step_reproducible():
     """Deterministic mode: two eager training steps from the same state and batch leave bit-identical
     BatchNorm running statistics (every statistic and BN-backward reduction is a fixed-order sum) and
@@ -326,7 +347,7 @@ def test_deterministic_step_reproducible():
     assert rel(u2, u1) < 1e-5, rel(u2, u1)
 
 
-def _graphed_vs_eager():
+def _graphed_vs_eager(two_stream: bool = False):
     from imagent_amd.data.loader import InputTransform
     from imagent_amd.models import resnet
     from imagent_amd.models.native import bind_native
@@ -349,7 +370,9 @@ def _graphed_vs_eager():
 
     def one(u8, y):
         runner.train_step([(tf(u8), y)])
-    step = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr)
+    step = GraphedStep(one, warmup=2, key_fn=lambda: opt.lr, two_stream=two_stream)
+    from imagent_amd.ops import streams
+    assert streams.overlap_enabled()  # (bind_native's default: weight gradients on the side stream)
     for i in range(3):  # 2 eager warm-up steps, then capture (+ replay)
         step(imgs[i], labs[i])
     assert step.graph is not None and step.replays == 1
