@@ -25,3 +25,13 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_sessionstart(session):
+    # IMAGENT_SEGV_BT=1: print native frames on SIGSEGV / SIGABRT (scripts/segv_bt.c), chained in front of
+    # pytest's faulthandler -- host-side diagnostics for crashes inside the HIP runtime (graph capture)
+    if os.environ.get("IMAGENT_SEGV_BT") == "1":
+        lib = os.path.join(ROOT, "scripts", "bin", "libsegv_bt.so")
+        if os.path.exists(lib):
+            import ctypes
+            ctypes.CDLL(lib).install()
