@@ -186,7 +186,7 @@ class BlockFn(torch.autograd.Function):
         side = streams.side_stream(x.device) if (ds is not None and x.is_cuda) else None
         ad = None
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
+            streams.wait(side, torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 ad = _fwd8(ds[0], x, x8, ds[1])
         xbn = [None] * len(pairs)  # xbn[i]: conv i applies the preceding BN + ReLU on its operand load
@@ -228,7 +228,7 @@ class BlockFn(torch.autograd.Function):
             if ds is not None:
                 if side is not None:
                     cur = torch.cuda.current_stream()
-                    cur.wait_stream(side)
+                    streams.wait(cur, side)
                     ad.record_stream(cur)
                 else:
                     ad = _fwd8(ds[0], x, x8, ds[1])
@@ -258,7 +258,7 @@ class BlockFn(torch.autograd.Function):
         elif ds is not None:
             if side is not None:
                 cur = torch.cuda.current_stream()
-                cur.wait_stream(side)
+                streams.wait(cur, side)
                 ad.record_stream(cur)  # allocated on the side stream, read / freed in main order
             else:
                 ad = _fwd8(ds[0], x, x8, ds[1])

@@ -174,7 +174,7 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
         raise ValueError("gram_wgrad needs bn (the block's bn3)")
     side = streams.side_stream(h2.device) if h2.is_cuda else None
     if side is not None:
-        side.wait_stream(torch.cuda.current_stream(h2.device))
+        streams.wait(side, torch.cuda.current_stream(h2.device))
     ctx = torch.cuda.stream(side) if side is not None else _Null()
     with ctx:
         C4, p = gb.g.shape[-1], h2.shape[-1]
@@ -191,6 +191,8 @@ def gram_wgrad(conv, gb: GramBN, h2: torch.Tensor, s: torch.Tensor = None, G: to
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record(side)
+                if torch.cuda.is_current_stream_capturing():
+                    streams._capture_events.append(ev)  # (waited on later; outlives the capture, streams.wait)
         if P is None:
             gram_G(h2, G)
         if own_s:

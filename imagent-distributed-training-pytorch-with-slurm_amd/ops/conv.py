@@ -428,7 +428,7 @@ def conv_wgrad(mod, dy: torch.Tensor, x: torch.Tensor, xbn: Optional[torch.Tenso
     if side is None:
         _conv_wgrad(mod, dy, x, xbn)
         return
-    side.wait_stream(torch.cuda.current_stream(dy.device))
+    streams.wait(side, torch.cuda.current_stream(dy.device))
     with torch.cuda.stream(side):
         _conv_wgrad(mod, dy, x, xbn)
     if xbn is not None:

@@ -179,7 +179,7 @@ class ConvF32Fn(torch.autograd.Function):
         g = mod.weight.grad.permute(0, 2, 3, 1)  # arena view, [Co][KH][KW][Ci] memory
         side = streams.side_stream(dy.device) if dy.is_cuda else None
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream(dy.device))
+            streams.wait(side, torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if x.shape[-1] != mod.in_channels:  # stem: 4-channel input, 3-channel weight
                 gp = torch.zeros_like(wk)
@@ -349,7 +349,7 @@ def _wgrad_side(mod, dy, x) -> None:
     """The weight gradient into the arena on the side stream (beside the rest of the backward)."""
     side = streams.side_stream(dy.device) if dy.is_cuda else None
     if side is not None:
-        side.wait_stream(torch.cuda.current_stream(dy.device))
+        streams.wait(side, torch.cuda.current_stream(dy.device))
     with torch.cuda.stream(side) if side is not None else _nullctx():
         g = mod.weight.grad.permute(0, 2, 3, 1)
         assert g.is_contiguous()

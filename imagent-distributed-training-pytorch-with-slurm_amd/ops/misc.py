@@ -139,7 +139,7 @@ class StemFn(torch.autograd.Function):
         streams.flush_deferred()  # layer1's conv1 weight gradient (queued behind this BN's backward)
         side = streams.side_stream(dy.device)
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream(dy.device))
+            streams.wait(side, torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(side) if side is not None else _NullCtx():
             gp = conv.grad_pad
             ok = stem_wgrad_bnx(g, img, gp, x, coef, conv.stride, conv.padding, conv.kh, conv.kw)

@@ -63,6 +63,31 @@ def active_side_stream() -> Optional[torch.cuda.Stream]:
 
 
 _keep: list = []
+# events of the fork / join edges recorded while a HIP graph is being captured: held until the capture has ended
+# (GraphedStep clears them). torch's Stream.wait_stream records a TEMPORARY event that is destroyed as soon as the
+# wait is enqueued; inside a two-stream capture on ROCm 7 that destroyed event is still referenced by the capture
+# and hipStreamEndCapture segfaulted (tests/test_model_gpu.py::test_graphed_two_stream_step_matches_eager)
+_capture_events: list = []
+
+
+def wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
+    """``dst`` waits for everything issued so far on ``src`` (Stream.wait_stream with an event that outlives a
+    capture in progress). A stream never waits on itself: eagerly that is a no-op, but inside a HIP graph capture
+    ROCm 7 turns the event wait into a self-edge of the captured graph, and hipStreamEndCapture's recursive walk
+    of the graph then recurses without end (the two-stream capture segfault of rounds 1 and 5: the reducer's
+    ``depend_on(side)`` issued from a weight-gradient launch already running ON the side stream; native
+    backtrace and HIP API log in profiles/r50_small_batch_graph_r6.md)."""
+    if dst.cuda_stream == src.cuda_stream:
+        return
+    ev = torch.cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
+    if torch.cuda.is_current_stream_capturing():
+        _capture_events.append(ev)
+
+
+def release_capture_events() -> None:
+    _capture_events.clear()
 # Side-stream operands are held until the end-of-backward join, then freed in
 # main-stream order (immediately reusable), rather than record_stream'ed (freed
 # only once the allocator sees the side stream pass them, so with the CPU ahead
@@ -85,7 +110,7 @@ def protect(*tensors: torch.Tensor) -> None:
 def join_side_into_current() -> None:
     s = active_side_stream()
     if s is not None:
-        torch.cuda.current_stream().wait_stream(s)
+        wait(torch.cuda.current_stream(), s)
     _keep.clear()
 
 

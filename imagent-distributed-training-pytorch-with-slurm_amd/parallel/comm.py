@@ -61,7 +61,8 @@ class Communicator:
     def depend_on(self, stream) -> None:
         """Collectives issued after this call also wait for ``stream``."""
         if torch.cuda.is_available():
-            torch.cuda.current_stream().wait_stream(stream)
+            from ..ops.streams import wait
+            wait(torch.cuda.current_stream(), stream)
 
 
 def stream_mode() -> int:

@@ -186,6 +186,7 @@ class GraphedStep:
                 self.fn(*self.static)
         finally:
             streams.set_wgrad_overlap(overlap)
+            streams.release_capture_events()  # the capture has ended: its fork / join events may go
         self.graph, self.key = g, key
         g.replay()  # the capture only recorded: run this step's work
         self.replays += 1

@@ -76,6 +76,7 @@ def main():
     loss_eager = met.reduced()[0]
     # graphed
     m, st, run, opt, met = build()
+    print(f"[repro] side stream enabled: {streams.overlap_enabled()}", flush=True)
     g = GraphedStep(lambda x, y: run.train_step([(x, y)]), warmup=2, key_fn=lambda: opt.lr,
                     two_stream=bool(a.two_stream))
     for i, (u8, y) in enumerate(batches):
