@@ -14,6 +14,9 @@
 //   -       bf16 weight shadows: [Co][T][Ci] -> [Ci][T][Co] for dgrad (batched)
 
 #include <cstdlib>
+#include <vector>
+
+#include <hip/hip_ext.h>
 
 #include "common.h"
 
@@ -972,3 +975,22 @@ IMK_EXPORT int imk_transpose_batched(const void* descs, int nd, int total_tiles,
 }
 
 IMK_EXPORT int imk_tdesc_size() { return (int)sizeof(TDesc); }
+
+// A stream restricted to `quarters` / 4 of the CUs (ops/streams.py IMAGENT_SIDE_CUMASK: the weight-gradient side
+// stream confined so that it cannot flood every CU while the main stream's critical-path kernels wait for slots).
+// CU i is enabled when (i / 8) % 4 < quarters: a quarter-pattern that is uniform over the 8 XCDs whether the mask bits
+// enumerate CUs XCD-major (i / 32 = XCD) or round-robin over XCDs (i % 8 = XCD). A CU-masked stream also gets a
+// hardware queue of its own. Kept for the process lifetime (never destroyed).
+IMK_EXPORT int imk_stream_create_cumask(int quarters, void** out) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (quarters < 1 || quarters > 4 || ncu <= 0) return -2;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i)
+        if ((i / 8) % 4 < quarters) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) return -3;
+    *out = (void*)s;
+    return 0;
+}

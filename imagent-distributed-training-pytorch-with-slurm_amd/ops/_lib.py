@@ -204,6 +204,7 @@ def _declare(name: str, lib) -> None:
             "imk_normalize_u8": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_resize_normalize_u8": [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
             "imk_transpose_batched": [vp, i32, i32, vp],
+            "imk_stream_create_cumask": [i32, C.POINTER(vp)],
             "imk_igemm_args_size": [], "imk_wgrad_args_size": [], "imk_bn_rundesc_size": [], "imk_bn_affdesc_size": [],
             "imk_tdesc_size": [], "imk_bn_bwd_scratch_floats": [i32],
             "imk_quant_fp8": [vp, vp, i64, vp, vp, vp],

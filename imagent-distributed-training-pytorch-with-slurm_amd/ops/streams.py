@@ -49,9 +49,27 @@ def side_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.St
     return s
 
 
+def side_cumask() -> int:
+    """IMAGENT_SIDE_CUMASK = q in 1..4: the side stream runs on q / 4 of the CUs (a CU-masked HIP stream,
+    ``imk_stream_create_cumask``); 0 (default): a plain stream over every CU. Measured at the 4096 default
+    (scripts/runs/cumask_ab.sh, one box): plain 17,500 / 17,471 img/s, q = 3 13,664 / 13,628, q = 2 13,310 / 13,314,
+    q = 1 10,434 -- the weight-gradient grids are sized for one wave over all 256 CUs, and the side stream's work is
+    90 ms of the 233 ms step: confined, it becomes the step's tail. Kept as an A/B switch only."""
+    import os
+    return int(os.environ.get("IMAGENT_SIDE_CUMASK", "0"))
+
+
 def _new_stream(idx: int):
     """A torch pool stream (normal priority: the alternatives measured slower, ``parallel/comm.py``
-    :func:`stream_mode`), kept for the process lifetime."""
+    :func:`stream_mode`), or a CU-masked one (:func:`side_cumask`), kept for the process lifetime."""
+    q = side_cumask()
+    if q:
+        import ctypes as C
+        from . import _lib
+        ptr = C.c_void_p()
+        with torch.cuda.device(idx):
+            _lib.check(_lib.kernels().imk_stream_create_cumask(q, C.byref(ptr)), "CU-masked side stream")
+        return torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", idx))
     return torch.cuda.Stream(device=idx)
 
 
