@@ -649,6 +649,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float qs0 = Q8 && g8.q[0] ? ldexpf(1.f, -g8.exp[0][0]) : 0.f;
     const float qs1 = Q8 && g8.q[1] ? ldexpf(1.f, -g8.exp[1][0]) : 0.f;
     float m0 = 0.f, m1 = 0.f;
+#ifdef IMAGENT_BN_DG_BLOCK0
     if (blockIdx.x == 0) {
         for (int c = tid; c < C; c += 256) {
             const bool sc = fold.slab != nullptr;
@@ -660,6 +661,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             }
         }
     }
+#else
+    // dgamma / dbeta accumulation spread over the first ceil(C / 256) blocks, one channel per thread, every operand
+    // loaded before the first store (formerly block 0 alone walked C / 256 iterations whose read-modify-writes the
+    // possible aliasing of dgamma / dbeta / scratch serialised into the pass's tail). scripts/runs/dg_ab.sh, one box:
+    // 256 img 12,922 / 12,941 vs 12,921 / 12,954 img/s (block 0 alone, -DIMAGENT_BN_DG_BLOCK0), 4096 img 17,312 vs
+    // 17,197 -- neutral at small batch, kept (no serial section left in the pass)
+    for (int c = blockIdx.x * 256 + tid; c < C; c += gridDim.x * 256) {
+        const bool sc = fold.slab != nullptr;
+        const float sgx = fld(scratch + sgxo + c, sc), sg = fld(scratch + C + c, sc);
+        const float sgx2 = MODE == 2 ? fld(scratch + 2 * C + c, sc) : 0.f;
+        const float og = dgamma ? dgamma[c] : 0.f, ob = dbeta ? dbeta[c] : 0.f;
+        const float og2 = MODE == 2 && dgamma2 ? dgamma2[c] : 0.f, ob2 = MODE == 2 && dbeta2 ? dbeta2[c] : 0.f;
+        if (dgamma) dgamma[c] = og + sgx;
+        if (dbeta) dbeta[c] = ob + sg;
+        if (MODE == 2) {
+            if (dgamma2) dgamma2[c] = og2 + sgx2;
+            if (dbeta2) dbeta2[c] = ob2 + sg;
+        }
+    }
+#endif
     if (tid >= rpb * cpr) return;
     const int ch = tid % cpr, c0 = ch * 8;
     float k1[8], kx[8], k0[8], q1[8], qx[8], q0[8], sc[8], sh[8];
