@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
 // instead -- a pixel only receives gradient as some window's argmax, so its
 // mask and x are that window's (the same sums, term for term): x (4x the
 // pooled bytes) is not read.
-template <int BNR>
+template <int BNR, bool NT = false>
 __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy,
                                                                const uint8_t* __restrict__ idx,
                                                                bf16_t* __restrict__ dx, int N, int C, int OH,
@@ -412,7 +412,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
                 u32x4 o;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) o[c] = pack_bf2(acc[2 * c], acc[2 * c + 1]);
-                *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + 2 * i + a) * W + 2 * j + b) * C + ch * 8) = o;
+                u32x4* dst = reinterpret_cast<u32x4*>(dx + (((size_t)n * H + 2 * i + a) * W + 2 * j + b) * C + ch * 8);
+                if (NT) __builtin_nontemporal_store(o, dst);
+                else *dst = o;
             }
     }
     if constexpr (BNR) {  // as maxpool_bwd_kernel: lane xor-fold, LDS adds, one atomic per channel
@@ -437,6 +439,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
         float* slot = bnr.slab + (size_t)(blockIdx.x & 31) * 3 * C;
         for (int c = threadIdx.x; c < 2 * C; c += 256) atomicAdd(slot + (c / C) * C + c % C, red[c / C][c % C]);
     }
+}
+
+// the quad backward's output (4x the bytes it reads) with non-temporal stores: scripts/pool_bench.py at 4096 img,
+// one box, twice each: 2,583 / 2,583 us plain vs 2,539 / 2,536 us NT (scripts/runs/pool_ab.sh). IMAGENT_POOL_NT=0: off
+static bool pool_nt() {
+    static const bool v = [] {
+        const char* e = getenv("IMAGENT_POOL_NT");
+        return e && *e ? atoi(e) != 0 : true;
+    }();
+    return v;
 }
 
 // the stem pool's quad-gather backward covers 3x3 / stride 2 / pad 1 on even inputs
@@ -764,7 +776,7 @@ IMK_EXPORT int imk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N,
     const long total = (long)N * H * W * (C / 8);
     if (total >= (1L << 32) - 8192L * 256) return -101;  // 32-bit index math
     if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
-        hipLaunchKernelGGL((maxpool_bwd_quad_kernel<0>), dim3(stream_grid(total / 4)), dim3(256), 0,
+        hipLaunchKernelGGL((pool_nt() ? maxpool_bwd_quad_kernel<0, true> : maxpool_bwd_quad_kernel<0, false>), dim3(stream_grid(total / 4)), dim3(256), 0,
                            (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
                            OW, PoolBnr{});
         IMK_CHECK_LAUNCH();
@@ -809,11 +821,11 @@ IMK_EXPORT int imk_maxpool_bwd_bnr(const void* dy, const void* idx, void* dx, co
     if (pool_quad_ok(H, W, OH, OW, k, s, p)) {
         const PoolBnr bnr{(const bf16_t*)x, save, gamma, beta, slab, (const bf16_t*)xsel};
         if (xsel)
-            hipLaunchKernelGGL((maxpool_bwd_quad_kernel<2>), dim3(stream_grid(total / 4)), dim3(256), 0,
+            hipLaunchKernelGGL((pool_nt() ? maxpool_bwd_quad_kernel<2, true> : maxpool_bwd_quad_kernel<2, false>), dim3(stream_grid(total / 4)), dim3(256), 0,
                                (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
                                OW, bnr);
         else
-            hipLaunchKernelGGL((maxpool_bwd_quad_kernel<1>), dim3(stream_grid(total / 4)), dim3(256), 0,
+            hipLaunchKernelGGL((pool_nt() ? maxpool_bwd_quad_kernel<1, true> : maxpool_bwd_quad_kernel<1, false>), dim3(stream_grid(total / 4)), dim3(256), 0,
                                (hipStream_t)stream, (const bf16_t*)dy, (const uint8_t*)idx, (bf16_t*)dx, N, C, OH,
                                OW, bnr);
         IMK_CHECK_LAUNCH();

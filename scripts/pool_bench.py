@@ -1,7 +1,10 @@
-"""Stand-alone timing of the stem pool's fused passes at the training shape (2048 x 112 x 112 x 64 -> 56 x 56):
-imk_maxpool_fwd_bn (with the per-window argmax input) and imk_maxpool_bwd_bnr from it.
+"""Isolated timing of the stem pool's fused passes (ops/misc.py StemFn): the BN + ReLU + 3x3/2 max-pool forward
+(imk_maxpool_fwd_bn, with the argmax-input copy xsel) and the quad-gather backward that stores the ReLU-masked BN
+upstream gradient and reduces the BN sums (imk_maxpool_bwd_bnr), ResNet-50 stem shapes at --batch images.
+us per call and HBM TB/s over the bytes each pass must move (inputs once, outputs once).
+IMAGENT_POOL_NT=0 / 1 selects the backward's plain / non-temporal (default) stores (A/B: one run per setting).
 
-python scripts/pool_bench.py --batch 2048
+python scripts/pool_bench.py [--batch 4096]
 """
 
 import argparse
@@ -13,54 +16,60 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 
+def timeit(fn, reps=10, warm=2):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=2048)
-    ap.add_argument("--reps", type=int, default=10)
-    a = ap.parse_args()
+    ap.add_argument("--batch", type=int, default=4096)
+    args = ap.parse_args()
     from imagent_amd.ops import _lib
     k = _lib.kernels()
-    dev = torch.device("cuda:0")
-    N, H, C, OH = a.batch, 112, 64, 56
+    dev = torch.device("cuda")
+    N, H, C = args.batch, 112, 64
+    OH = 56
+    torch.manual_seed(0)
     x = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
-    sums = torch.stack([torch.zeros(C, device=dev), torch.ones(C, device=dev)]).contiguous()
-    gamma, beta = torch.ones(C, device=dev), torch.zeros(C, device=dev)
-    save = torch.empty(2, C, device=dev)
+    sums = torch.zeros(2, C, device=dev)
+    sums[1] = 1.0  # (mean 0, variance 1)
+    gamma = torch.ones(C, device=dev)
+    beta = torch.zeros(C, device=dev)
+    save = torch.zeros(2, C, device=dev)
     y = torch.empty(N, OH, OH, C, device=dev, dtype=torch.bfloat16)
-    idx = torch.empty(y.shape, device=dev, dtype=torch.uint8)
+    idx = torch.empty(N, OH, OH, C, device=dev, dtype=torch.uint8)
     xsel = torch.empty_like(y)
-    dy = torch.randn(y.shape, device=dev).to(torch.bfloat16)
-    g = torch.empty_like(x)
-    slab = torch.zeros(32, 3, C, device=dev)
     st = _lib.stream_ptr()
-    spin = torch.randn(4096, 4096, device=dev)
-    for _ in range(30):
-        spin = spin @ spin
-        spin /= spin.norm()
 
     def fwd():
         _lib.check(k.imk_maxpool_fwd_bn(x.data_ptr(), sums.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                                         save.data_ptr(), y.data_ptr(), idx.data_ptr(), xsel.data_ptr(), N, H, H, C,
-                                        OH, OH, 3, 2, 1, 1e-5, st), "fwd")
+                                        OH, OH, 3, 2, 1, 1e-5, st), "pool fwd")
+    fwd()
+    dy = torch.randn_like(y)
+    g = torch.empty_like(x)
+    slab = torch.zeros(k.imk_bn_bwd_scratch_floats(C), device=dev)  # the BN's backward scratch
 
     def bwd():
         _lib.check(k.imk_maxpool_bwd_bnr(dy.data_ptr(), idx.data_ptr(), g.data_ptr(), x.data_ptr(), xsel.data_ptr(),
-                                         save.data_ptr(), gamma.data_ptr(), beta.data_ptr(), slab.data_ptr(), N, H,
-                                         H, C, OH, OH, 3, 2, 1, st), "bwd")
-    big = N * H * H * C * 2
-    nb = big + big // 4 * 2 + big // 8  # fwd: x in, y + xsel + idx out; bwd: g out, dy + xsel + idx in
-    for name, fn in (("pool_fwd_bn", fwd), ("pool_bwd_bnr", bwd)):
-        for _ in range(2):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.reps):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1000 / a.reps
-        print(f"{name:14s} {us:8.1f} us  {nb / us / 1e6:5.2f} TB/s", flush=True)
+                                         save.data_ptr(), gamma.data_ptr(), beta.data_ptr(), slab.data_ptr(), N, H, H,
+                                         C, OH, OH, 3, 2, 1, st), "pool bwd")
+    xb, yb = x.numel() * 2, y.numel() * 2
+    tf = timeit(fwd)
+    tb = timeit(bwd)
+    fb = xb + 2 * yb + yb // 2        # x in; y, xsel, idx out
+    bb = 2 * yb + yb // 2 + xb        # dy, xsel, idx in; g out
+    print(f"batch {N} pool_nt={os.environ.get('IMAGENT_POOL_NT', '1')}: fwd {tf:8.1f} us {fb / tf / 1e6:5.2f} TB/s | "
+          f"bwd {tb:8.1f} us {bb / tb / 1e6:5.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":
