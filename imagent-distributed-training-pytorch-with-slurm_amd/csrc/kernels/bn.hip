@@ -196,7 +196,14 @@ __device__ __forceinline__ void fold_wait(const SlabFold& f, int n) {
 
 // a folded value: sc1 (agent-scope relaxed) load when it was published inside this launch, else a plain load
 __device__ __forceinline__ float fld(const float* p, bool sc) {
+#ifdef IMAGENT_BN_APPLY_SERIAL
     return sc ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+#else
+    // always the sc1 load: an L2-coherent read is as valid for a value written before the launch, and a runtime
+    // choice between two loads made every per-channel constant a branch with its own load and wait
+    (void)sc;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // ---------------------------------------------------------------- forward
@@ -717,10 +724,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
             if (MODE == 2) x2v[u] = ldwn<NTL>(x2 + off);
             if (MASK == 1) yv[u] = ldwn<NTL>(y + off);
         }
+#ifndef IMAGENT_BN_APPLY_SERIAL
+        // every row's loads stay issued before any math: left alone, the compiler sank the loads of rows 1..U-1 below
+        // the previous row's `r >= R` exit, so a wave had ONE row (g, x) in flight -- load, wait, math, store, next
+        // row (the forward pass kept its U rows). An empty asm that takes every loaded chunk as a register operand pins
+        // the loads above it (one wait for all of them); the rows past R compute on clamped loads and are not stored.
+        // scripts/runs/apply_ab.sh, one box: per-step apply passes at 256 img 3,511 -> 3,038 us, bench.py 256 img
+        // 12,992 -> 13,369 / 13,370 img/s, 4096 img 17,183 / 17,221 -> 17,227 / 17,273 (2048-img passes isolated +1.7 %)
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            asm volatile("" ::"v"(g[u]), "v"(xv[u]));
+            if (MODE == 2) asm volatile("" ::"v"(x2v[u]));
+            if (MASK == 1) asm volatile("" ::"v"(yv[u]));
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const long r = r0 + u * step;
+#ifdef IMAGENT_BN_APPLY_SERIAL
             if (r >= R) break;
+#else
+            if (r >= R) continue;
+#endif
             const size_t off = (size_t)r * C + c0;
             float gv[8], o[8];
 #pragma unroll
@@ -802,9 +827,14 @@ static int apply_bpc() {
     static const int v = env_int("IMAGENT_BN_APPLY_BPC", 4);
     return v;
 }
-static bool apply_ntload() {
+// Non-temporal loads only for tensors past the MALL's reach: at 256 img (scripts/runs/bn_small.sh, tensors of 13-103 MB
+// that the producing kernel has just written) plain loads took the per-step apply passes 3,506 -> 3,389 us (512@7
+// 25.5 -> 22.4 us, the mode-2 2048@7 79.2 -> 60.7 us); NT wins on the GB-sized tensors of 2048-4096 img (above).
+// IMAGENT_BN_NTLOAD_MIN_MB: smallest tensor (MB) that takes NT loads.
+static bool apply_ntload(long R, int C) {
     static const bool v = env_int("IMAGENT_BN_NTLOAD", 1) != 0;
-    return v;
+    static const long min_bytes = (long)env_int("IMAGENT_BN_NTLOAD_MIN_MB", 256) << 20;
+    return v && R * (long)C * 2 >= min_bytes;
 }
 static int n_cus() {
     static const int n = [] {
@@ -913,6 +943,8 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     // fold_in: the apply pass folds the slab itself (SlabFold; its counter in the scratch's last row), else one
     // launch of its own
     SlabFold fold{};
+    static const bool fold_ok = env_int("IMAGENT_BN_FOLD_IN", 1) != 0;  // 0: the separate fold launch (A/B)
+    fold_in = fold_in && fold_ok;
     if (fold_in) {
         fold = SlabFold{scratch, nullptr, folded, reinterpret_cast<uint32_t*>(folded + 3 * C), BWD_SLOTS, 0.f};
     } else {
@@ -922,7 +954,7 @@ IMK_EXPORT int imk_bn_bwd_apply(const void* g, const void* x, const float* save,
     }
     const int grid = std::max(std::min(grid_for(R, C), apply_bpc() * n_cus()), fold_in ? (3 * C + 255) / 256 : 1);
     const float inv_cnt = 1.f / (float)R;
-    const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1], ntl = apply_ntload();
+    const bool nt = bn_nt(), q8 = g8.q[0] || g8.q[1], ntl = apply_ntload(R, C);
 #define LK(M, NT, Q8, NTL)                                                                           \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<0, M, NT, Q8, NTL>),                                          \
                        dim3(resident_grid((const void*)bn_bwd_apply_kernel<0, M, NT, Q8, NTL>, grid)), dim3(256), 0, st, (const bf16_t*)g, \
