@@ -827,13 +827,13 @@ static int apply_bpc() {
     static const int v = env_int("IMAGENT_BN_APPLY_BPC", 4);
     return v;
 }
-// Non-temporal loads only for tensors past the MALL's reach: at 256 img (scripts/runs/bn_small.sh, tensors of 13-103 MB
-// that the producing kernel has just written) plain loads took the per-step apply passes 3,506 -> 3,389 us (512@7
-// 25.5 -> 22.4 us, the mode-2 2048@7 79.2 -> 60.7 us); NT wins on the GB-sized tensors of 2048-4096 img (above).
-// IMAGENT_BN_NTLOAD_MIN_MB: smallest tensor (MB) that takes NT loads.
+// Non-temporal loads at every size by default: with the loads batched, plain loads below 256 MB per tensor won
+// isolated at 256 img (scripts/bn_bench.py, operands still cached from the previous call: apply passes 3,036 ->
+// 2,915 us per step) but lost in-step (bench.py 256 img 13,492 / 13,510 NT vs 13,453 / 13,427 img/s,
+// scripts/runs/ntmin_ab.sh). IMAGENT_BN_NTLOAD_MIN_MB: smallest tensor (MB) that takes NT loads (A/B).
 static bool apply_ntload(long R, int C) {
     static const bool v = env_int("IMAGENT_BN_NTLOAD", 1) != 0;
-    static const long min_bytes = (long)env_int("IMAGENT_BN_NTLOAD_MIN_MB", 256) << 20;
+    static const long min_bytes = (long)env_int("IMAGENT_BN_NTLOAD_MIN_MB", 0) << 20;
     return v && R * (long)C * 2 >= min_bytes;
 }
 static int n_cus() {

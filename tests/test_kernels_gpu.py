@@ -596,6 +596,28 @@ def test_normalize_and_transpose():
     assert torch.equal(d, c.permute(2, 1, 0))
 
 
+@pytest.mark.parametrize("W,Cp", [(40, 4), (36, 8), (38, 4), (38, 8)])
+def test_normalize_quad_and_per_pixel_paths(W, Cp):
+    """The 4-pixel normalize kernel (W % 4 == 0, Cp 4 / 8) and the per-pixel one (W = 38) against torch, with
+    per-sample crops and flips."""
+    from imagent_amd.ops.misc import normalize_u8
+    torch.manual_seed(7)
+    img = torch.randint(0, 256, (4, 41, 47, 3), dtype=torch.uint8, device=DEV)
+    crop = torch.tensor([[1, 2], [0, 0], [5, 7], [9, 47 - W]], dtype=torch.int32, device=DEV)
+    flip = torch.tensor([0, 1, 1, 0], dtype=torch.uint8, device=DEV)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    out = normalize_u8(img, (32, W), Cp, mean, std, crop, flip).float()
+    ref = torch.zeros(4, 32, W, Cp, device=DEV)
+    for b in range(4):
+        oy, ox = crop[b].tolist()
+        t = img[b, oy:oy + 32, ox:ox + W].float() / 255
+        if flip[b]:
+            t = t.flip(1)
+        ref[b, ..., :3] = (t - torch.tensor(mean, device=DEV)) / torch.tensor(std, device=DEV)
+    assert (out - ref).abs().max().item() < 0.02  # bf16 rounding of values up to |2.6|
+    assert torch.equal(out[..., 3:], torch.zeros_like(out[..., 3:]))
+
+
 def test_fp8_quant_matches_torch_e4m3():
     from imagent_amd.ops.fp8 import ActScales, WeightQuantizer, quant_act
     torch.manual_seed(8)
