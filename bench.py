@@ -343,7 +343,15 @@ def main(argv=None):
             print(json.dumps(out), flush=True)
         comm.close()
 
-    run()
+    # IMAGENT_MAIN_PRIO=1 (A/B): the whole step on a high-priority stream, so that the critical-path kernels'
+    # workgroups are dispatched ahead of the weight-gradient side stream's as CU slots free up. Measured slower
+    # (4096 img 17,639 / 17,712 -> 16,981 / 16,962 img/s, 256 img 13,547 -> 9,328: profiles/ab/prio_r6.txt)
+    if on_gpu and os.environ.get("IMAGENT_MAIN_PRIO", "0") == "1":
+        hp = torch.cuda.Stream(device=ctx.device, priority=min(torch.cuda.Stream.priority_range()))
+        with torch.cuda.stream(hp):
+            run()
+    else:
+        run()
     ctx.shutdown()
 
 
