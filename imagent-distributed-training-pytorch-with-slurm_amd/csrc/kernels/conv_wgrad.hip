@@ -317,13 +317,22 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     if (a.Ci % 8 || a.Co % 8) return -100;
     // LDS-DMA main loop (conv_wgrad_v3.h) for the 1x1 convs it covers (conv_bench at 1024 img: 1x1
     // wgrads -790 us per step in total, e.g. 512 -> 256 @28 457 -> 325 us; on 3x3 the register-staged
-    // kernel stays ahead, 128 @28 452 vs 497). IMAGENT_WGRAD_V3 = 0 off, 1 (default) 1x1 with 64-row
-    // stages x 2, 2: 64 x 3, 3: 32 x 4, 4: 128 x 2, 5: 64 x 2 for every shape it covers
+    // kernel stays ahead, 128 @28 452 vs 497). IMAGENT_WGRAD_V3 = 0 off, 1: 1x1 with 64-row stages x 2, 2: 64 x 3,
+    // 3: 32 x 4, 4: 128 x 2, 5: 64 x 2 for every shape it covers, 6 (default): 1x1 and the 3x3 shapes the halo kernel
+    // below does not take (stride 2, 7x7 maps) instead of the register-staged loop. Isolated, the register-staged loop
+    // is 4-15 % ahead on those 3x3 shapes (round 5, below); in-step on the side stream the LDS-DMA loop wins: 4096 img
+    // 17,276 / 17,257 -> 17,354 / 17,330 img/s, 256 img 13,535 -> 13,567 (round 6, scripts/runs/wgv3_ab.sh, every
+    // production shape's numerics in tests/test_conv_shapes_gpu.py)
     static const int v3 = [] {
         const char* e = getenv("IMAGENT_WGRAD_V3");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 6;
     }();
-    if (v3 && wgrad_v3_ok(a) && (v3 == 5 || (a.KH == 1 && a.KW == 1))) {
+    static const int halo_mode = [] {
+        const char* e = getenv("IMAGENT_WGRAD_HALO");
+        return e ? atoi(e) : 2;
+    }();
+    const bool v3_rest = v3 == 6 && !(halo_mode && wgrad_halo_ok(a, halo_mode >= 2, true));
+    if (v3 && wgrad_v3_ok(a) && (v3 == 5 || v3_rest || (a.KH == 1 && a.KW == 1))) {
         switch (v3) {
             case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
             case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
