@@ -331,8 +331,10 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
         const char* e = getenv("IMAGENT_WGRAD_HALO");
         return e ? atoi(e) : 2;
     }();
-    const bool v3_rest = v3 == 6 && !(halo_mode && wgrad_halo_ok(a, halo_mode >= 2, true));
+    // 7 (A/B): as 6, with the 256 x 256 tile (16 waves, one block per CU) wherever it covers the shape
+    const bool v3_rest = (v3 == 6 || v3 == 7) && !(halo_mode && wgrad_halo_ok(a, halo_mode >= 2, true));
     if (v3 && wgrad_v3_ok(a) && (v3 == 5 || v3_rest || (a.KH == 1 && a.KW == 1))) {
+        if (v3 == 7 && wgrad_v3w_ok<4, 4>(a)) return launch_wgrad_v3<64, 2, 4, 4>(a, 0, st);  // (its own split count)
         switch (v3) {
             case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
             case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
