@@ -331,10 +331,21 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
         const char* e = getenv("IMAGENT_WGRAD_HALO");
         return e ? atoi(e) : 2;
     }();
-    // 7 (A/B): as 6, with the 256 x 256 tile (16 waves, one block per CU) wherever it covers the shape
+    // 6 also takes the 256 x 256 tile (16 waves, one block per CU, its own split count) when the step is large:
+    // at least IMAGENT_WGRAD_WIDE_MIN_IMAGES images per GPU (default 2048); 7 (A/B): wherever it covers the shape.
+    // In-step, one box each (scripts/runs/wgv7_ab.sh, wide_ab.sh): everywhere at 4096 img 17,419 / 17,392 ->
+    // 17,672 / 17,702 img/s and 17,533 -> 17,786 / 17,782; at 256 img 13,510 -> 13,171, by a per-shape row bound
+    // (>= 200,704 pixels: layers 1-2 at 256 img) 13,435 / 13,448 -> 13,386 / 13,390 -- the 128-KB blocks keep the
+    // small main-stream kernels of a small step from co-residing (round 5's note above imk_conv_wgrad_variant), so
+    // the bound is on the step size; at 2048 img round 5 measured the tile neutral in-step
+    static const long wide_min = [] {
+        const char* e = getenv("IMAGENT_WGRAD_WIDE_MIN_IMAGES");
+        return e ? atol(e) : 2048L;
+    }();
     const bool v3_rest = (v3 == 6 || v3 == 7) && !(halo_mode && wgrad_halo_ok(a, halo_mode >= 2, true));
     if (v3 && wgrad_v3_ok(a) && (v3 == 5 || v3_rest || (a.KH == 1 && a.KW == 1))) {
-        if (v3 == 7 && wgrad_v3w_ok<4, 4>(a)) return launch_wgrad_v3<64, 2, 4, 4>(a, 0, st);  // (its own split count)
+        if ((v3 == 7 || (v3 == 6 && (long)a.N >= wide_min)) && wgrad_v3w_ok<4, 4>(a))
+            return launch_wgrad_v3<64, 2, 4, 4>(a, 0, st);
         switch (v3) {
             case 2: return launch_wgrad_v3<64, 3>(a, splits, st);
             case 3: return launch_wgrad_v3<32, 4>(a, splits, st);
