@@ -65,8 +65,12 @@ _GRAM_NOX = os.environ.get("IMAGENT_BN_GRAM", "1") != "slab"
 # loses (same-box A/B: ResNet-152 at 256 img/GPU 4,699 img/s with every block in the Gram form vs 5,080 without,
 # at 1024 img/GPU 6,279 vs 6,019; ResNet-50 at 256 11,636 vs 12,097)
 _GRAM_MIN_ROWS = int(os.environ.get("IMAGENT_GRAM_MIN_ROWS", "100000"))
-# IMAGENT_DS_SIDE=0 (A/B): the downsample conv's forward on the main stream instead of beside the main chain
-_DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "1") != "0"
+# the downsample conv's forward on the main stream (default) or, IMAGENT_DS_SIDE=1, on the side stream beside the
+# main chain's BN passes (rounds 2-5): at 4096 img the side placement lost in 5 of 5 alternating pairs, +0.1-1.0 %
+# for the main stream (scripts/runs/ds_ab.sh, ds_ab2.sh; profiles/ab/ds_side_r6.txt) -- the side stream's
+# concurrent work slows the memory-bound main-chain kernels more than the overlap gains (profiles/
+# instep_contention_r6.md); neutral at 256 img
+_DS_SIDE = os.environ.get("IMAGENT_DS_SIDE", "0") == "1"
 # ... and bottleneck widths p <= 256: the extension grows as p^2 M against ~32 M p bytes saved, and at p = 512
 # (ResNet-50's layer 4) it loses at the same per-block work where p = 256 wins (same-box A/B at 2048 img/GPU, where
 # layer 4 passes the row bound: 16,620 / 16,610 img/s without its Gram form vs 16,543 / 16,529 with it; layer 3 at
@@ -183,8 +187,8 @@ class BlockFn(torch.autograd.Function):
         saved = [x]
         h, h8 = x, x8
         ds = block.downsample
-        # the downsample conv depends only on x: on the (idle in forward) side stream it
-        # runs beside the main chain's memory-bound BN passes
+        # the downsample conv depends only on x: with IMAGENT_DS_SIDE=1 it runs on the (idle in forward) side stream
+        # beside the main chain's memory-bound BN passes (off by default, see _DS_SIDE)
         side = streams.side_stream(x.device) if (ds is not None and x.is_cuda and _DS_SIDE) else None
         ad = None
         if side is not None:
