@@ -141,9 +141,13 @@ def test_hip_training_variants_learn(tmp_path, extra):
 
 def test_bn_shift_off_switch_trains(tmp_path):
     """IMAGENT_BN_SHIFT=0 (forward BN statistics as raw sums, an A/B switch): the finalize must not
-    add the previous batch mean back (it did: NaN losses from the second step on)."""
-    out = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "3", "--synthetic-train-size", str(32 * 40)],
+    add the previous batch mean back (it did: NaN losses from the second step on).
+    Epochs of 40 steps, the decay after epoch 2 as the other tests, and TWO epochs at lr 0.005: with one, a
+    late-round-6 run passed through an lr-0.05 loss spike in epoch 2 (validation loss 40, the chaotic regime of the
+    module docstring) and its 40 steps at 0.005 recovered to 68.5 % only -- the same check on the last epoch, with
+    the low-lr phase long enough to follow the trajectory back out of a spike."""
+    out = _run(BASE + DECAY + ["--kernels", "hip", "--epochs", "4", "--synthetic-train-size", str(32 * 40)],
                tmp_path, IMAGENT_BN_SHIFT="0")
     summ, top1 = _curve(out)
-    assert len(summ) == 3, out[-2000:]
+    assert len(summ) == 4, out[-2000:]
     _learned(summ, top1, out)
