@@ -257,7 +257,13 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
         // one wave of blocks over 256 CUs (two per CU for the 4-wave tile): the 1x1 wgrads are split-K streams whose
         // second, partial wave of blocks cost more than the extra atomics of deeper splits save (same-box bench:
         // 512 blocks 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282)
-        constexpr int target = WCO * WKC == 4 ? 512 : 256;
+        // (16-wave tile: IMAGENT_WGRAD_WIDE_TARGET blocks, A/B -- fewer than one per CU leaves CUs to the main
+        // stream's small kernels, which otherwise wait for a slot behind the one-block-per-CU side-stream grid)
+        static const int wide_target = [] {
+            const char* e = getenv("IMAGENT_WGRAD_WIDE_TARGET");
+            return e && atoi(e) > 0 ? atoi(e) : 256;
+        }();
+        const int target = WCO * WKC == 4 ? 512 : wide_target;
         const int want = (target + ntiles - 1) / ntiles;
         const int maxs = (a.M + 4 * BR - 1) / (4 * BR);
         splits = max(1, min(want, maxs));
