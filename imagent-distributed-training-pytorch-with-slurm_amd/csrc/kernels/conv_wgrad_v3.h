@@ -258,7 +258,8 @@ int launch_wgrad_v3(WgradArgs a, int splits, hipStream_t st) {
         // second, partial wave of blocks cost more than the extra atomics of deeper splits save (same-box bench:
         // 512 blocks 15,314 / 15,357 img/s, 768 15,291, 1024 15,287 / 15,303, 1536 15,282)
         // (16-wave tile: IMAGENT_WGRAD_WIDE_TARGET blocks, A/B -- fewer than one per CU leaves CUs to the main
-        // stream's small kernels, which otherwise wait for a slot behind the one-block-per-CU side-stream grid)
+        // stream's small kernels, which otherwise wait for a slot behind the one-block-per-CU side-stream grid; measured
+        // at 4096 img: 256 17,899 / 17,805, 192 17,805 / 17,790, 128 17,749 / 17,755 img/s -- one per CU stays)
         static const int wide_target = [] {
             const char* e = getenv("IMAGENT_WGRAD_WIDE_TARGET");
             return e && atoi(e) > 0 ? atoi(e) : 256;
