@@ -327,7 +327,7 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
         const char* e = getenv("IMAGENT_WGRAD_V3");
         return e ? atoi(e) : 6;
     }();
-    static const int halo_mode = [] {
+    static const int halo_mode = [] {  // IMAGENT_WGRAD_HALO, see the halo-kernel branch below
         const char* e = getenv("IMAGENT_WGRAD_HALO");
         return e ? atoi(e) : 2;
     }();
@@ -355,10 +355,7 @@ IMK_EXPORT int imk_conv_wgrad(const WgradArgs* args, int splits, void* stream) {
     }
     // 3x3 stride-1 with 64-channel slices: the halo-tiled kernel (conv_wgrad_halo.h); IMAGENT_WGRAD_HALO=0 off,
     // 1 only 64 -> 64, 2 (default) every shape it covers
-    static const int halo = [] {
-        const char* e = getenv("IMAGENT_WGRAD_HALO");
-        return e ? atoi(e) : 2;
-    }();
+    const int halo = halo_mode;  // (read once above)
     if (halo && wgrad_halo_ok(a, halo >= 2, true)) return launch_wgrad_halo(a, st);
     if (a.Co <= 64) return launch<64, 128, 1, false>(a, splits, st);
     // (an LDS-DMA ring variant with a 2*(row&7)-swizzled 256-B-row image measured
